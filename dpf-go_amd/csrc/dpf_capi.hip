@@ -1,0 +1,381 @@
+// dpf_capi.hip — the C ABI (include/dpf_hip.h) over the gfx950 kernels.
+//
+// Host-buffer entry points stage keys into HBM, run the kernels on a
+// per-device stream under a per-device mutex and copy results back;
+// device-resident (_dev) entry points only enqueue on the caller's stream.
+// There is no CPU evaluation path: without a usable gfx950 device every
+// evaluation call fails with DPF_ERR_NODEV.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/dpf_hip.h"
+#include "dpf_internal.hpp"
+#include "dpf_kernels.hpp"
+
+using dpfh::full_len;
+using dpfh::key_len;
+using dpfh::stop_of;
+
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int code, const std::string& msg) {
+    t_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) return fail(DPF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Dev {
+    int id = 0;
+    hipStream_t st = nullptr;
+    std::mutex mu;
+    DevBuf keys, work, out, xs;
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<Dev>> g_devs;
+
+// Largest output slab staged in HBM per launch by the host-buffer paths.
+constexpr size_t kMaxSlab = (size_t)1 << 30;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(d);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int open_devices(int ngpus) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_devs.empty()) return (int)g_devs.size();
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return fail(DPF_ERR_NODEV, "dpf: no HIP device visible (gfx950 required)");
+    if (ngpus > 0) n = std::min(n, ngpus);
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, i) != hipSuccess) return fail(DPF_ERR_NODEV, "dpf: device query failed");
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(DPF_ERR_NODEV, std::string("dpf: device is ") + prop.gcnArchName + ", need gfx950");
+    }
+    for (int i = 0; i < n; ++i) {
+        auto d = std::make_unique<Dev>();
+        d->id = i;
+        DeviceGuard g(i);
+        if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess)
+            return fail(DPF_ERR_HIP, "dpf: hipStreamCreate failed");
+        g_devs.push_back(std::move(d));
+    }
+    return n;
+}
+
+int ensure_open() {
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_devs.empty()) return (int)g_devs.size();
+    }
+    return open_devices(0);
+}
+
+int check_key(size_t klen, uint32_t logN) {
+    if (logN > 63) return fail(DPF_ERR_PARAM, "dpf: logN > 63");
+    if (klen < key_len(logN)) return fail(DPF_ERR_KEYLEN, "dpf: key shorter than 33+18*(logN-7) bytes");
+    return DPF_OK;
+}
+
+// Evaluate subtree (prefix_bits, prefix) of nk keys already resident at
+// d_keys into d_out (2^(stop-prefix_bits) leaves per key), on stream st.
+int enqueue_full(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t logN, uint32_t prefix_bits,
+                 uint64_t prefix, uint8_t* d_out, uint32_t* d_work, hipStream_t st) {
+    const uint32_t stop = stop_of(logN);
+    HIP_TRY(dpfk::launch_unpack(d_keys, klen, nk, stop, d_work, st));
+    const uint64_t stride = (uint64_t)16 << (stop - prefix_bits);
+    HIP_TRY(dpfk::launch_evalfull(d_work, nk, stop, prefix_bits, prefix, d_out, stride, st));
+    return DPF_OK;
+}
+
+// Host-buffer EvalFull of keys [0, nk) on one device, output slab-chunked.
+int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t logN, uint8_t* out) {
+    std::lock_guard<std::mutex> lk(d.mu);
+    DeviceGuard g(d.id);
+    const uint32_t stop = stop_of(logN);
+    const size_t olen = full_len(logN);
+    if (olen <= kMaxSlab) {
+        const size_t per = std::max<size_t>(1, kMaxSlab / olen);
+        for (size_t k0 = 0; k0 < nk; k0 += per) {
+            const size_t n = std::min(per, nk - k0);
+            HIP_TRY(hipError_t(d.keys.ensure(n * klen)));
+            HIP_TRY(hipError_t(d.work.ensure(n * dpfk::ek_words(stop) * 4)));
+            HIP_TRY(hipError_t(d.out.ensure(n * olen)));
+            HIP_TRY(hipMemcpyAsync(d.keys.p, keys + k0 * klen, n * klen, hipMemcpyHostToDevice, d.st));
+            int rc = enqueue_full((const uint8_t*)d.keys.p, klen, n, logN, 0, 0, (uint8_t*)d.out.p,
+                                  (uint32_t*)d.work.p, d.st);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(out + k0 * olen, d.out.p, n * olen, hipMemcpyDeviceToHost, d.st));
+            HIP_TRY(hipStreamSynchronize(d.st));
+        }
+        return DPF_OK;
+    }
+    // One key's output exceeds a slab: walk it subtree by subtree.
+    uint32_t pb = 0;
+    while ((olen >> pb) > kMaxSlab) ++pb;
+    const size_t slab = olen >> pb;
+    HIP_TRY(hipError_t(d.keys.ensure(klen)));
+    HIP_TRY(hipError_t(d.work.ensure(dpfk::ek_words(stop) * 4)));
+    HIP_TRY(hipError_t(d.out.ensure(slab)));
+    for (size_t k = 0; k < nk; ++k) {
+        HIP_TRY(hipMemcpyAsync(d.keys.p, keys + k * klen, klen, hipMemcpyHostToDevice, d.st));
+        for (uint64_t p = 0; p < (1ull << pb); ++p) {
+            int rc = enqueue_full((const uint8_t*)d.keys.p, klen, 1, logN, pb, p, (uint8_t*)d.out.p,
+                                  (uint32_t*)d.work.p, d.st);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(out + k * olen + p * slab, d.out.p, slab, hipMemcpyDeviceToHost, d.st));
+            HIP_TRY(hipStreamSynchronize(d.st));
+        }
+    }
+    return DPF_OK;
+}
+
+int eval_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, const uint64_t* xs, size_t ppk,
+                   uint32_t logN, uint8_t* out) {
+    std::lock_guard<std::mutex> lk(d.mu);
+    DeviceGuard g(d.id);
+    const uint32_t stop = stop_of(logN);
+    const size_t nq = nk * ppk;
+    HIP_TRY(hipError_t(d.keys.ensure(std::max<size_t>(1, nk * klen))));
+    HIP_TRY(hipError_t(d.work.ensure(std::max<size_t>(1, nk * dpfk::ek_words(stop) * 4))));
+    HIP_TRY(hipError_t(d.xs.ensure(std::max<size_t>(8, nq * 8))));
+    HIP_TRY(hipError_t(d.out.ensure(std::max<size_t>(1, nq))));
+    HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
+    HIP_TRY(hipMemcpyAsync(d.xs.p, xs, nq * 8, hipMemcpyHostToDevice, d.st));
+    HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, nk, stop, (uint32_t*)d.work.p, d.st));
+    HIP_TRY(dpfk::launch_eval((const uint32_t*)d.work.p, stop, logN, (const uint64_t*)d.xs.p, nq, ppk,
+                              (uint8_t*)d.out.p, d.st));
+    HIP_TRY(hipMemcpyAsync(out, d.out.p, nq, hipMemcpyDeviceToHost, d.st));
+    HIP_TRY(hipStreamSynchronize(d.st));
+    return DPF_OK;
+}
+
+// Run fn(device_index, lo, hi) over `n` items split evenly across g devices.
+template <class F>
+int shard(size_t n, int g, F fn) {
+    if (g <= 1 || n <= 1) return fn(0, (size_t)0, n);
+    std::vector<int> rc((size_t)g, DPF_OK);
+    std::vector<std::string> errs((size_t)g);
+    std::vector<std::thread> th;
+    for (int i = 0; i < g; ++i) {
+        const size_t lo = n * (size_t)i / (size_t)g, hi = n * (size_t)(i + 1) / (size_t)g;
+        th.emplace_back([&, i, lo, hi] {
+            rc[(size_t)i] = lo < hi ? fn(i, lo, hi) : DPF_OK;
+            errs[(size_t)i] = t_err;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int i = 0; i < g; ++i)
+        if (rc[(size_t)i]) return fail(rc[(size_t)i], errs[(size_t)i]);
+    return DPF_OK;
+}
+
+int pick_ngpus(int ngpus) {
+    int have = ensure_open();
+    if (have <= 0) return have;
+    return ngpus <= 0 ? have : std::min(ngpus, have);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dpf_last_error(void) { return t_err.c_str(); }
+
+size_t dpf_key_len(uint32_t logN) { return key_len(logN); }
+size_t dpf_evalfull_len(uint32_t logN) { return full_len(logN); }
+size_t dpf_workspace_size(size_t nkeys, uint32_t logN) {
+    return std::max<size_t>(16, nkeys * dpfk::ek_words(stop_of(logN)) * 4);
+}
+
+int dpf_gpu_init(int ngpus) { return open_devices(ngpus); }
+
+void dpf_gpu_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& d : g_devs) {
+        std::lock_guard<std::mutex> dl(d->mu);
+        DeviceGuard g(d->id);
+        (void)hipStreamSynchronize(d->st);
+        d->keys.release();
+        d->work.release();
+        d->out.release();
+        d->xs.release();
+        (void)hipStreamDestroy(d->st);
+    }
+    g_devs.clear();
+}
+
+int dpf_gpu_count(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return (int)g_devs.size();
+}
+
+int dpf_gen_seeded(uint64_t alpha, uint32_t logN, const uint8_t s0[16], const uint8_t s1[16], uint8_t* ka,
+                   uint8_t* kb) {
+    int rc = dpfh::gen_seeded(alpha, logN, s0, s1, ka, kb);
+    return rc ? fail(rc, "dpf: invalid parameters") : DPF_OK;
+}
+
+int dpf_gen(uint64_t alpha, uint32_t logN, uint8_t* ka, uint8_t* kb) {
+    int rc = dpfh::gen_random(alpha, logN, ka, kb);
+    return rc ? fail(rc, "dpf: invalid parameters") : DPF_OK;
+}
+
+int dpf_gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, const uint8_t* s1s, size_t n,
+                         uint8_t* kas, uint8_t* kbs, int nthreads) {
+    int rc = dpfh::gen_batch_seeded(alphas, logN, s0s, s1s, n, kas, kbs, nthreads);
+    return rc ? fail(rc, "dpf: invalid parameters") : DPF_OK;
+}
+
+int dpf_evalfull_batch(const uint8_t* keys, size_t klen, size_t nkeys, uint32_t logN, uint8_t* out, int ngpus) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const int g = pick_ngpus(ngpus);
+    if (g <= 0) return g;
+    const size_t olen = full_len(logN);
+    return shard(nkeys, g, [&](int dev, size_t lo, size_t hi) {
+        return full_on_device(*g_devs[(size_t)dev], keys + lo * klen, klen, hi - lo, logN, out + lo * olen);
+    });
+}
+
+int dpf_evalfull(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out) {
+    return dpf_evalfull_batch(key, klen, 1, logN, out, 1);
+}
+
+int dpf_eval_batch(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_t* xs, size_t ppk, uint32_t logN,
+                   uint8_t* out, int ngpus) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const int g = pick_ngpus(ngpus);
+    if (g <= 0) return g;
+    return shard(nkeys, g, [&](int dev, size_t lo, size_t hi) {
+        return eval_on_device(*g_devs[(size_t)dev], keys + lo * klen, klen, hi - lo, xs + lo * ppk, ppk, logN,
+                              out + lo * ppk);
+    });
+}
+
+int dpf_eval(const uint8_t* key, size_t klen, uint64_t x, uint32_t logN, uint8_t* out_bit) {
+    return dpf_eval_batch(key, klen, 1, &x, 1, logN, out_bit, 1);
+}
+
+int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out, int ngpus) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const int have = pick_ngpus(ngpus);
+    if (have <= 0) return have;
+    const uint32_t stop = stop_of(logN);
+    const int want = ngpus <= 0 ? have : ngpus;
+    if (want > have) return fail(DPF_ERR_PARAM, "dpf: more GPUs requested than opened");
+    uint32_t pb = 0;
+    while ((1 << pb) < want) ++pb;
+    if ((1 << pb) != want || pb > stop) return fail(DPF_ERR_PARAM, "dpf: ngpus must be a power of two <= 2^(logN-7)");
+    const size_t slab = full_len(logN) >> pb;
+    return shard((size_t)want, want, [&](int dev, size_t lo, size_t hi) {
+        (void)hi;
+        Dev& d = *g_devs[(size_t)dev];
+        std::lock_guard<std::mutex> lk(d.mu);
+        DeviceGuard gd(d.id);
+        HIP_TRY(hipError_t(d.keys.ensure(klen)));
+        HIP_TRY(hipError_t(d.work.ensure(dpfk::ek_words(stop) * 4)));
+        HIP_TRY(hipError_t(d.out.ensure(slab)));
+        HIP_TRY(hipMemcpyAsync(d.keys.p, key, klen, hipMemcpyHostToDevice, d.st));
+        int rc = enqueue_full((const uint8_t*)d.keys.p, klen, 1, logN, pb, lo, (uint8_t*)d.out.p,
+                              (uint32_t*)d.work.p, d.st);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(out + lo * slab, d.out.p, slab, hipMemcpyDeviceToHost, d.st));
+        HIP_TRY(hipStreamSynchronize(d.st));
+        return DPF_OK;
+    });
+}
+
+int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN,
+                             uint32_t prefix_bits, uint64_t prefix, uint8_t* d_out, void* d_work, void* stream) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const uint32_t stop = stop_of(logN);
+    if (prefix_bits > stop || (prefix_bits < 64 && (prefix >> prefix_bits) != 0))
+        return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
+    if (nkeys == 0) return DPF_OK;
+    DeviceGuard g(device);
+    return enqueue_full(d_keys, klen, nkeys, logN, prefix_bits, prefix, d_out, (uint32_t*)d_work,
+                        (hipStream_t)stream);
+}
+
+int dpf_evalfull_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN,
+                           uint8_t* d_out, void* d_work, void* stream) {
+    return dpf_evalfull_subtree_dev(device, d_keys, klen, nkeys, logN, 0, 0, d_out, d_work, stream);
+}
+
+int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, const uint64_t* d_xs,
+                       size_t ppk, uint32_t logN, uint8_t* d_out, void* d_work, void* stream) {
+    if (int rc = check_key(klen, logN)) return rc;
+    if (nkeys == 0 || ppk == 0) return DPF_OK;
+    const uint32_t stop = stop_of(logN);
+    DeviceGuard g(device);
+    HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop, (uint32_t*)d_work, (hipStream_t)stream));
+    HIP_TRY(dpfk::launch_eval((const uint32_t*)d_work, stop, logN, d_xs, nkeys * ppk, ppk, d_out,
+                              (hipStream_t)stream));
+    return DPF_OK;
+}
+
+int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN, void* d_work,
+                        void* stream) {
+    if (int rc = check_key(klen, logN)) return rc;
+    DeviceGuard g(device);
+    HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop_of(logN), (uint32_t*)d_work, (hipStream_t)stream));
+    return DPF_OK;
+}
+
+int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
+                              uint64_t prefix, uint8_t* d_out, void* stream) {
+    if (logN > 63) return fail(DPF_ERR_PARAM, "dpf: logN > 63");
+    const uint32_t stop = stop_of(logN);
+    if (prefix_bits > stop || (prefix >> prefix_bits) != 0) return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
+    if (nkeys == 0) return DPF_OK;
+    DeviceGuard g(device);
+    const uint64_t stride = (uint64_t)16 << (stop - prefix_bits);
+    HIP_TRY(dpfk::launch_evalfull((const uint32_t*)d_work, nkeys, stop, prefix_bits, prefix, d_out, stride,
+                                  (hipStream_t)stream));
+    return DPF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,18 @@
+// dpf_internal.hpp — shared declarations inside libdpf_hip.so.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dpfh {
+
+inline uint32_t stop_of(uint32_t logN) { return logN >= 7 ? logN - 7 : 0; }
+inline size_t key_len(uint32_t logN) { return 33 + 18 * (size_t)stop_of(logN); }
+inline size_t full_len(uint32_t logN) { return logN >= 7 ? ((size_t)1 << (logN - 3)) : 16; }
+
+bool host_has_aesni();
+int gen_seeded(uint64_t alpha, uint32_t logN, const uint8_t s0[16], const uint8_t s1[16], uint8_t* ka, uint8_t* kb);
+int gen_random(uint64_t alpha, uint32_t logN, uint8_t* ka, uint8_t* kb);
+int gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, const uint8_t* s1s, size_t n,
+                     uint8_t* kas, uint8_t* kbs, int nthreads);
+
+}  // namespace dpfh

@@ -1,0 +1,26 @@
+// dpf_kernels.hpp — launchers for the gfx950 DPF kernels (dpf_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpfk {
+
+constexpr int kBlock = 512;    // threads per workgroup (8 waves); 2 workgroups per CU (64 KiB LDS table each)
+constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
+
+// Expanded-key words per key: (stop + 2) records of 8 u32.
+inline uint64_t ek_words(uint32_t stop) { return ((uint64_t)stop + 2) * 8; }
+
+hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ek,
+                         hipStream_t st);
+
+// EvalFull of the subtree rooted at depth `prefix_bits`, index `prefix`, of
+// every key (prefix_bits = 0 -> whole domain).  Output per key: 2^(stop -
+// prefix_bits) leaves of 16 B at out + key * out_stride.
+hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
+                           uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st);
+
+hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
+                       uint64_t pts_per_key, uint8_t* out, hipStream_t st);
+
+}  // namespace dpfk

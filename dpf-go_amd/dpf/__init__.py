@@ -1,0 +1,252 @@
+"""dpf — Python mirror of dkales/dpf-go's package ``dpf`` over libdpf_hip.so.
+
+Same names, argument meaning and error behaviour as the Go API
+(/root/reference/dpf/dpf.go):
+
+    Gen(alpha, logN)   -> (ka, kb)     dpf.go:71   (host; seeds from getrandom)
+    Eval(k, x, logN)   -> 0 | 1        dpf.go:171  (gfx950 kernel)
+    EvalFull(k, logN)  -> bytes        dpf.go:243  (gfx950 kernel)
+
+Where Go panics, these raise ``DPFPanic`` ("dpf: invalid parameters" for Gen,
+dpf.go:72-74).  Batched and device-resident forms are added for the engine.
+
+There is no CPU evaluation path: the HIP library must be built
+(``make -C dpf-go_amd``) and a gfx950 device must be visible, otherwise
+evaluation raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdpf_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "dpf_hip.h")
+
+DPF_OK = 0
+DPF_ERR_PARAM = -1
+DPF_ERR_KEYLEN = -2
+DPF_ERR_NODEV = -3
+DPF_ERR_HIP = -4
+DPF_ERR_NOMEM = -5
+
+
+class DPFPanic(RuntimeError):
+    """Raised where the Go reference panics (or the device path fails)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg or f"dpf: error {code}")
+        self.code = code
+
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_sz = ctypes.c_size_t
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must cover every function in include/dpf_hip.h
+SIGNATURES = {
+    "dpf_last_error": (ctypes.c_char_p, []),
+    "dpf_key_len": (_sz, [_u32]),
+    "dpf_evalfull_len": (_sz, [_u32]),
+    "dpf_workspace_size": (_sz, [_sz, _u32]),
+    "dpf_gpu_init": (_int, [_int]),
+    "dpf_gpu_shutdown": (None, []),
+    "dpf_gpu_count": (_int, []),
+    "dpf_gen_seeded": (_int, [_u64, _u32, _u8p, _u8p, _u8p, _u8p]),
+    "dpf_gen": (_int, [_u64, _u32, _u8p, _u8p]),
+    "dpf_gen_batch_seeded": (_int, [_u64p, _u32, _u8p, _u8p, _sz, _u8p, _u8p, _int]),
+    "dpf_eval": (_int, [_u8p, _sz, _u64, _u32, _u8p]),
+    "dpf_evalfull": (_int, [_u8p, _sz, _u32, _u8p]),
+    "dpf_evalfull_batch": (_int, [_u8p, _sz, _sz, _u32, _u8p, _int]),
+    "dpf_eval_batch": (_int, [_u8p, _sz, _sz, _u64p, _sz, _u32, _u8p, _int]),
+    "dpf_evalfull_split": (_int, [_u8p, _sz, _u32, _u8p, _int]),
+    "dpf_evalfull_batch_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp, _vp]),
+    "dpf_evalfull_subtree_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _vp, _vp]),
+    "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _vp]),
+    "dpf_expand_keys_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp]),
+    "dpf_evalfull_expanded_dev": (_int, [_int, _vp, _sz, _u32, _u32, _u64, _vp, _vp]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libdpf_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: build it with `make -C dpf-go_amd` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != DPF_OK:
+        msg = lib().dpf_last_error().decode(errors="replace")
+        raise DPFPanic(rc, msg)
+
+
+def _buf(a: np.ndarray):
+    return a.ctypes.data_as(_u8p)
+
+
+def _as_u8(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8)
+    return np.frombuffer(bytes(b), dtype=np.uint8)
+
+
+def key_len(logN: int) -> int:
+    return int(lib().dpf_key_len(logN))
+
+
+def evalfull_len(logN: int) -> int:
+    return int(lib().dpf_evalfull_len(logN))
+
+
+def workspace_size(nkeys: int, logN: int) -> int:
+    return int(lib().dpf_workspace_size(nkeys, logN))
+
+
+def gpu_init(ngpus: int = 0) -> int:
+    rc = lib().dpf_gpu_init(ngpus)
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+def gpu_shutdown() -> None:
+    lib().dpf_gpu_shutdown()
+
+
+# ------------------------------------------------------------------ Gen ---
+def gen_seeded(alpha: int, logN: int, s0: bytes, s1: bytes) -> Tuple[bytes, bytes]:
+    """Gen with the two crypto/rand seeds (dpf.go:80-81) supplied."""
+    if logN > 63 or logN < 0 or alpha < 0 or alpha >= (1 << logN):
+        raise DPFPanic(DPF_ERR_PARAM, "dpf: invalid parameters")
+    n = key_len(logN)
+    ka = np.zeros(n, np.uint8)
+    kb = np.zeros(n, np.uint8)
+    _check(lib().dpf_gen_seeded(alpha, logN, _buf(_as_u8(s0)), _buf(_as_u8(s1)), _buf(ka), _buf(kb)))
+    return ka.tobytes(), kb.tobytes()
+
+
+def Gen(alpha: int, logN: int) -> Tuple[bytes, bytes]:
+    """dpf.go:71 — two key shares for the point function at alpha."""
+    if logN > 63 or logN < 0 or alpha < 0 or alpha >= (1 << logN):
+        raise DPFPanic(DPF_ERR_PARAM, "dpf: invalid parameters")
+    n = key_len(logN)
+    ka = np.zeros(n, np.uint8)
+    kb = np.zeros(n, np.uint8)
+    _check(lib().dpf_gen(alpha, logN, _buf(ka), _buf(kb)))
+    return ka.tobytes(), kb.tobytes()
+
+
+def gen_batch_seeded(alphas: Sequence[int], logN: int, s0s: np.ndarray, s1s: np.ndarray,
+                     nthreads: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """Batched seeded Gen on host threads -> (ka[n, klen], kb[n, klen])."""
+    al = np.ascontiguousarray(alphas, dtype=np.uint64)
+    n = al.shape[0]
+    s0 = np.ascontiguousarray(s0s, dtype=np.uint8).reshape(n, 16)
+    s1 = np.ascontiguousarray(s1s, dtype=np.uint8).reshape(n, 16)
+    kl = key_len(logN)
+    ka = np.zeros((n, kl), np.uint8)
+    kb = np.zeros((n, kl), np.uint8)
+    _check(lib().dpf_gen_batch_seeded(al.ctypes.data_as(_u64p), logN, _buf(s0), _buf(s1), n, _buf(ka), _buf(kb),
+                                      nthreads))
+    return ka, kb
+
+
+# ----------------------------------------------------------- evaluation ---
+def Eval(k: bytes, x: int, logN: int) -> int:
+    """dpf.go:171 — the share of f_alpha(x), 0 or 1."""
+    kk = _as_u8(k)
+    out = np.zeros(1, np.uint8)
+    _check(lib().dpf_eval(_buf(kk), kk.size, x & 0xFFFFFFFFFFFFFFFF, logN, _buf(out)))
+    return int(out[0])
+
+
+def EvalFull(key: bytes, logN: int) -> bytes:
+    """dpf.go:243 — the share of f_alpha over the whole domain, packed bits."""
+    kk = _as_u8(key)
+    out = np.zeros(evalfull_len(logN), np.uint8)
+    _check(lib().dpf_evalfull(_buf(kk), kk.size, logN, _buf(out)))
+    return out.tobytes()
+
+
+def evalfull_batch(keys: np.ndarray, logN: int, ngpus: int = 0) -> np.ndarray:
+    """keys[n, klen] uint8 -> out[n, evalfull_len(logN)] uint8."""
+    kk = np.ascontiguousarray(keys, dtype=np.uint8)
+    n, kl = kk.shape
+    out = np.zeros((n, evalfull_len(logN)), np.uint8)
+    _check(lib().dpf_evalfull_batch(_buf(kk), kl, n, logN, _buf(out), ngpus))
+    return out
+
+
+def eval_batch(keys: np.ndarray, xs: np.ndarray, logN: int, ngpus: int = 0) -> np.ndarray:
+    """keys[n, klen], xs[n, p] uint64 -> out[n, p] uint8 (0/1)."""
+    kk = np.ascontiguousarray(keys, dtype=np.uint8)
+    x = np.ascontiguousarray(xs, dtype=np.uint64)
+    n, kl = kk.shape
+    p = x.shape[1]
+    out = np.zeros((n, p), np.uint8)
+    _check(lib().dpf_eval_batch(_buf(kk), kl, n, x.ctypes.data_as(_u64p), p, logN, _buf(out), ngpus))
+    return out
+
+
+def evalfull_split(key: bytes, logN: int, ngpus: int) -> bytes:
+    kk = _as_u8(key)
+    out = np.zeros(evalfull_len(logN), np.uint8)
+    _check(lib().dpf_evalfull_split(_buf(kk), kk.size, logN, _buf(out), ngpus))
+    return out.tobytes()
+
+
+# --------------------------------------------- device-resident (torch) ---
+def _ptr(t) -> int:
+    return int(t.data_ptr())
+
+
+def _stream_handle(stream) -> int:
+    return int(stream.cuda_stream) if stream is not None else 0
+
+
+def evalfull_batch_dev(d_keys, key_len_: int, nkeys: int, logN: int, d_out, d_work, device: int = 0,
+                       stream=None) -> None:
+    """Enqueue EvalFull of nkeys HBM-resident keys on `stream` (torch stream)."""
+    _check(lib().dpf_evalfull_batch_dev(device, _ptr(d_keys), key_len_, nkeys, logN, _ptr(d_out), _ptr(d_work),
+                                        _stream_handle(stream)))
+
+
+def evalfull_subtree_dev(d_keys, key_len_: int, nkeys: int, logN: int, prefix_bits: int, prefix: int, d_out,
+                         d_work, device: int = 0, stream=None) -> None:
+    _check(lib().dpf_evalfull_subtree_dev(device, _ptr(d_keys), key_len_, nkeys, logN, prefix_bits, prefix,
+                                          _ptr(d_out), _ptr(d_work), _stream_handle(stream)))
+
+
+def eval_batch_dev(d_keys, key_len_: int, nkeys: int, d_xs, pts_per_key: int, logN: int, d_out, d_work,
+                   device: int = 0, stream=None) -> None:
+    _check(lib().dpf_eval_batch_dev(device, _ptr(d_keys), key_len_, nkeys, _ptr(d_xs), pts_per_key, logN,
+                                    _ptr(d_out), _ptr(d_work), _stream_handle(stream)))
+
+
+def expand_keys_dev(d_keys, key_len_: int, nkeys: int, logN: int, d_work, device: int = 0, stream=None) -> None:
+    _check(lib().dpf_expand_keys_dev(device, _ptr(d_keys), key_len_, nkeys, logN, _ptr(d_work),
+                                     _stream_handle(stream)))
+
+
+def evalfull_expanded_dev(d_work, nkeys: int, logN: int, d_out, prefix_bits: int = 0, prefix: int = 0,
+                          device: int = 0, stream=None) -> None:
+    _check(lib().dpf_evalfull_expanded_dev(device, _ptr(d_work), nkeys, logN, prefix_bits, prefix, _ptr(d_out),
+                                           _stream_handle(stream)))

@@ -1,0 +1,113 @@
+/*
+ * dpf_hip.h — C ABI of the MI355X DPF evaluation engine (libdpf_hip.so).
+ *
+ * Drop-in boundary for dkales/dpf-go's evaluation path.  The reference's Go
+ * API is (dpf/dpf.go):
+ *     type DPFkey []byte                                  :7
+ *     func Gen(alpha, logN uint64) (DPFkey, DPFkey)       :71
+ *     func Eval(k DPFkey, x, logN uint64) byte            :171
+ *     func EvalFull(key DPFkey, logN uint64) []byte       :243
+ * A cgo file in package dpf keeps those signatures and calls the functions
+ * below.  Byte layouts are the reference's, unchanged:
+ *   key   = seed[16] | t[1] | stop x (sCW[16] | tLCW[1] | tRCW[1]) | finalCW[16]
+ *           stop = max(logN-7, 0), length 33 + 18*stop      (dpf.go:89-167)
+ *   EvalFull output = 2^(logN-3) bytes (16 if logN < 7), point x is bit
+ *           (x % 8) of byte (x / 8)                          (dpf.go:248-251, dpf_test.go:52)
+ *
+ * Conventions: every buffer is caller-owned; calls are synchronous unless
+ * the name ends in _dev; nothing is retained after return (cgo pointer
+ * rules).  Return value 0 = success, negative = error (DPF_ERR_*); the Go
+ * wrapper turns a nonzero code into panic(), as the reference panics.
+ * All functions are thread-safe (per-device mutex + stream).
+ */
+#ifndef DPF_HIP_H
+#define DPF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPF_OK 0
+#define DPF_ERR_PARAM (-1)   /* invalid alpha/logN: where Gen panics (dpf.go:72-74) */
+#define DPF_ERR_KEYLEN (-2)  /* key shorter than 33+18*stop: where Eval/EvalFull index out of range */
+#define DPF_ERR_NODEV (-3)   /* no usable gfx950 device / dpf_gpu_init not possible */
+#define DPF_ERR_HIP (-4)     /* HIP runtime error (message in dpf_last_error) */
+#define DPF_ERR_NOMEM (-5)   /* device or host allocation failed */
+
+/* Last error message of the calling thread ("" if none). */
+const char* dpf_last_error(void);
+
+/* ---- sizes ------------------------------------------------------------ */
+/* len(DPFkey) produced by Gen for this logN (dpf.go:89-167). */
+size_t dpf_key_len(uint32_t logN);
+/* len(EvalFull(k, logN)) (dpf.go:248-251). */
+size_t dpf_evalfull_len(uint32_t logN);
+/* Device scratch bytes the _dev entry points need for nkeys keys. */
+size_t dpf_workspace_size(size_t nkeys, uint32_t logN);
+
+/* ---- device management (no reference counterpart: the reference has no
+ *      device; dpf.go:22-44 init() is the nearest analogue) --------------- */
+/* Open ngpus devices (<= 0: every visible device).  Idempotent.  Returns the
+ * number of devices opened (> 0) or a negative error. */
+int dpf_gpu_init(int ngpus);
+void dpf_gpu_shutdown(void);
+int dpf_gpu_count(void);
+
+/* ---- host-side key generation (Gen stays on the host, north star) ------ */
+/* Replaces Gen (dpf.go:71-169) with the two crypto/rand seeds (:80-81)
+ * passed in.  ka/kb: dpf_key_len(logN) bytes each. */
+int dpf_gen_seeded(uint64_t alpha, uint32_t logN, const uint8_t s0[16], const uint8_t s1[16], uint8_t* ka,
+                   uint8_t* kb);
+/* Gen (dpf.go:71) itself: seeds from getrandom(2), like crypto/rand. */
+int dpf_gen(uint64_t alpha, uint32_t logN, uint8_t* ka, uint8_t* kb);
+/* n keys pairs at once over nthreads host threads (<= 0: all cores).
+ * alphas[n], s0s/s1s [n][16], kas/kbs [n][dpf_key_len]. */
+int dpf_gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, const uint8_t* s1s, size_t n,
+                         uint8_t* kas, uint8_t* kbs, int nthreads);
+
+/* ---- evaluation, host buffers (synchronous; PCIe-inclusive) ------------ */
+/* Eval (dpf.go:171-211): *out_bit = 0/1. */
+int dpf_eval(const uint8_t* key, size_t key_len, uint64_t x, uint32_t logN, uint8_t* out_bit);
+/* EvalFull (dpf.go:243-262): out = dpf_evalfull_len(logN) bytes. */
+int dpf_evalfull(const uint8_t* key, size_t key_len, uint32_t logN, uint8_t* out);
+/* nkeys x EvalFull; keys packed [nkeys][key_len], out [nkeys][evalfull_len].
+ * Keys are sharded over ngpus devices (<= 0: all opened devices). */
+int dpf_evalfull_batch(const uint8_t* keys, size_t key_len, size_t nkeys, uint32_t logN, uint8_t* out, int ngpus);
+/* nkeys x pts_per_key Eval; xs [nkeys][pts_per_key], out one 0/1 byte per
+ * query in the same order. */
+int dpf_eval_batch(const uint8_t* keys, size_t key_len, size_t nkeys, const uint64_t* xs, size_t pts_per_key,
+                   uint32_t logN, uint8_t* out, int ngpus);
+/* One EvalFull split by top-level subtree over ngpus devices (ngpus must be
+ * a power of two <= 2^stop); out = dpf_evalfull_len(logN) bytes. */
+int dpf_evalfull_split(const uint8_t* key, size_t key_len, uint32_t logN, uint8_t* out, int ngpus);
+
+/* ---- evaluation, device-resident buffers (asynchronous on `stream`) ----
+ * Pointers are device pointers on `device`; `work` holds
+ * dpf_workspace_size(nkeys, logN) bytes; stream is a hipStream_t (NULL =
+ * the default stream).  Nothing is synchronised. */
+int dpf_evalfull_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, uint32_t logN,
+                           uint8_t* d_out, void* d_work, void* stream);
+/* The subtree at depth prefix_bits, index prefix of every key: 2^(logN-3-
+ * prefix_bits) bytes per key at d_out + k*that (logN-7 >= prefix_bits). */
+int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, uint32_t logN,
+                             uint32_t prefix_bits, uint64_t prefix, uint8_t* d_out, void* d_work, void* stream);
+int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, const uint64_t* d_xs,
+                       size_t pts_per_key, uint32_t logN, uint8_t* d_out, void* d_work, void* stream);
+
+/* Two-phase form of the above: expand keys once into d_work (the aligned
+ * per-level records the kernels read), then evaluate any number of
+ * subtrees from the expanded form.  Lets a caller time the tree kernel
+ * alone and reuse expanded keys across calls. */
+int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, uint32_t logN, void* d_work,
+                        void* stream);
+int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
+                              uint64_t prefix, uint8_t* d_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DPF_HIP_H */
