@@ -4,12 +4,18 @@
 // and the PRG dpf/dpf.go:59-69 over aes128MMO (dpf/aes_amd64.s:51-82).
 //
 // PRG back end ("T-table"): AES-128 as four lookups per column into Te0 held
-// in LDS, one private copy per lane of the wave: entry e of lane l lives at
-// byte e*256 + 4*l, so a wave's 64 lookups always hit 64 distinct banks
-// (conflict-free at any index pattern) and the LDS address of byte k of a
-// column is a single v_perm_b32 {0, 0, x.byte_k, 4*lane}.  Te1..Te3 are
-// rotations (v_alignbit).  Round keys are compile-time literals: the two PRG
-// keys are fixed (dpf/dpf.go:23-24).
+// in LDS.  Row e (256 B) holds 32 lane copies of Te0[e] followed by 32 copies
+// of rotl8(Te0[e]); lane l reads copy (l mod 32) at byte e*256 + 4*(l mod 32)
+// (+128 for the rotated word).  ds_read_b32 serves each 32-lane half in one
+// pass over banks (a/4) mod 32, so every lookup is conflict-free whatever the
+// indices.  The LDS address of byte k of a column is one v_perm_b32
+// {0, 0, x.byte_k, lane offset}.  With the rotated copy a column needs one
+// rotation instead of three:
+//   out = Ta ^ R8Tb ^ R16(Tc ^ R8Td) ^ rk.
+// v_perm / v_alignbit issue at ~0.6x the rate of v_xor / v_bitop3 on gfx950
+// (tools/valu_peak.hip), so rotations and address math dominate the VALU
+// budget.  Round keys are compile-time literals: the two PRG keys are fixed
+// (dpf/dpf.go:23-24).
 //
 // Tree: a thread owns a subtree of 2^D leaves (D <= 7).  It walks from the
 // root to its subtree root computing only the child on its path (one AES per
@@ -30,8 +36,16 @@ struct Blk {
 };
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+constexpr uint32_t crotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 
-// LDS address of Te0[byte K of x] in this lane's copy.
+// v_bitop3_b32 truth tables (src0 = 0xF0, src1 = 0xCC, src2 = 0xAA).
+constexpr uint32_t kXor3 = 0x96;     // a ^ b ^ c
+constexpr uint32_t kOrXor = 0x56;    // (a | b) ^ c
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, kXor3);
+}
+
+// LDS address of the Te0 pair for byte K of x in this lane's copy.
 template <int K>
 __device__ __forceinline__ uint32_t taddr(uint32_t x, uint32_t laneoff) {
     // v_perm_b32 selector: result byte0 = src1.byte0 (lane offset), byte1 =
@@ -39,18 +53,25 @@ __device__ __forceinline__ uint32_t taddr(uint32_t x, uint32_t laneoff) {
     return __builtin_amdgcn_perm(x, laneoff, 0x0c0c0000u | ((4u + K) << 8));
 }
 
-template <int K>
+// Te0[x.byte K] (ROT = false) or rotl8(Te0[x.byte K]) (ROT = true).
+template <int K, bool ROT = false>
 __device__ __forceinline__ uint32_t tl(const uint8_t* tab, uint32_t x, uint32_t laneoff) {
-    return *reinterpret_cast<const uint32_t*>(tab + taddr<K>(x, laneoff));
+    return *reinterpret_cast<const uint32_t*>(tab + taddr<K>(x, laneoff) + (ROT ? 128 : 0));
 }
 
 // Round-key sources.  KeyFixed<R>: the fixed left/right PRG key (literal).
 // KeySel: per-lane choice, rk = rkL ^ (m & (rkL ^ rkR)), m = 0 or ~0.
+// get16<I>() = rotl(rk_I, 16), folded into the pre-rotation XOR of a column.
 template <bool RIGHT>
 struct KeyFixed {
     template <int I>
     __device__ __forceinline__ uint32_t get() const {
         return RIGHT ? dpfc::kRkR.w[I] : dpfc::kRkL.w[I];
+    }
+    template <int I>
+    __device__ __forceinline__ uint32_t get16() const {
+        constexpr uint32_t v = crotl(RIGHT ? dpfc::kRkR.w[I] : dpfc::kRkL.w[I], 16);
+        return v;
     }
 };
 struct KeySel {
@@ -61,18 +82,27 @@ struct KeySel {
         constexpr uint32_t d = dpfc::kRkL.w[I] ^ dpfc::kRkR.w[I];
         return l ^ (m & d);
     }
+    template <int I>
+    __device__ __forceinline__ uint32_t get16() const {
+        constexpr uint32_t l = crotl(dpfc::kRkL.w[I], 16);
+        constexpr uint32_t d = crotl(dpfc::kRkL.w[I] ^ dpfc::kRkR.w[I], 16);
+        return l ^ (m & d);
+    }
 };
 
 template <int R, class K>
 __device__ __forceinline__ void aes_round(const uint8_t* tab, uint32_t lo, const K& k, Blk& s) {
-    uint32_t n0 = tl<0>(tab, s.c0, lo) ^ rotl(tl<1>(tab, s.c1, lo), 8) ^ rotl(tl<2>(tab, s.c2, lo), 16) ^
-                  rotl(tl<3>(tab, s.c3, lo), 24) ^ k.template get<4 * R + 0>();
-    uint32_t n1 = tl<0>(tab, s.c1, lo) ^ rotl(tl<1>(tab, s.c2, lo), 8) ^ rotl(tl<2>(tab, s.c3, lo), 16) ^
-                  rotl(tl<3>(tab, s.c0, lo), 24) ^ k.template get<4 * R + 1>();
-    uint32_t n2 = tl<0>(tab, s.c2, lo) ^ rotl(tl<1>(tab, s.c3, lo), 8) ^ rotl(tl<2>(tab, s.c0, lo), 16) ^
-                  rotl(tl<3>(tab, s.c1, lo), 24) ^ k.template get<4 * R + 2>();
-    uint32_t n3 = tl<0>(tab, s.c3, lo) ^ rotl(tl<1>(tab, s.c0, lo), 8) ^ rotl(tl<2>(tab, s.c1, lo), 16) ^
-                  rotl(tl<3>(tab, s.c2, lo), 24) ^ k.template get<4 * R + 3>();
+    // column j: Te0[s_j.b0] ^ Te1[s_{j+1}.b1] ^ Te2[s_{j+2}.b2] ^ Te3[s_{j+3}.b3] ^ rk_j, Te_i = rotl(Te0, 8i)
+    // = Ta ^ R8Tb ^ R16(Tc ^ R8Td ^ R16 rk): two v_bitop3 + one v_alignbit.
+    auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t rk16) {
+        uint32_t ta = tl<0>(tab, a, lo), tb = tl<1, true>(tab, b, lo), tc = tl<2>(tab, c, lo),
+                 td = tl<3, true>(tab, d, lo);
+        return xor3(ta, tb, rotl(xor3(tc, td, rk16), 16));
+    };
+    uint32_t n0 = col(s.c0, s.c1, s.c2, s.c3, k.template get16<4 * R + 0>());
+    uint32_t n1 = col(s.c1, s.c2, s.c3, s.c0, k.template get16<4 * R + 1>());
+    uint32_t n2 = col(s.c2, s.c3, s.c0, s.c1, k.template get16<4 * R + 2>());
+    uint32_t n3 = col(s.c3, s.c0, s.c1, s.c2, k.template get16<4 * R + 3>());
     s.c0 = n0; s.c1 = n1; s.c2 = n2; s.c3 = n3;
 }
 
@@ -83,7 +113,7 @@ __device__ __forceinline__ void aes_last(const uint8_t* tab, uint32_t lo, const 
         uint32_t la = tl<0>(tab, a, lo), lb = tl<1>(tab, b, lo), lc = tl<2>(tab, c, lo), ld = tl<3>(tab, d, lo);
         uint32_t p = __builtin_amdgcn_perm(lb, la, 0x0c0c0501u);   // {la.b1, lb.b1, 0, 0}
         uint32_t q = __builtin_amdgcn_perm(ld, lc, 0x05010c0cu);   // {0, 0, lc.b1, ld.b1}
-        return (p | q) ^ rk;
+        return __builtin_amdgcn_bitop3_b32(p, q, rk, kOrXor);
     };
     uint32_t n0 = col(s.c0, s.c1, s.c2, s.c3, k.template get<40>());
     uint32_t n1 = col(s.c1, s.c2, s.c3, s.c0, k.template get<41>());
@@ -241,10 +271,11 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
 }
 
 __device__ __forceinline__ void fill_table(uint32_t* tab) {
-    // 256 entries x 64 lane copies; each thread writes 16-byte runs.
+    // Row e: 32 copies of Te0[e], then 32 copies of rotl8(Te0[e]); 16-byte stores.
     for (uint32_t i = threadIdx.x; i < 256 * 16; i += blockDim.x) {
         uint32_t e = i >> 4, q = i & 15;
         uint32_t v = c_te0.v[e];
+        if (q >= 8) v = rotl(v, 8);
         reinterpret_cast<uint4*>(tab)[e * 16 + q] = make_uint4(v, v, v, v);
     }
     __syncthreads();
@@ -297,7 +328,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_evalfull(const uint32_t* __restri
 
     Ctx c;
     c.tab = reinterpret_cast<const uint8_t*>(s_tab);
-    c.lo = (threadIdx.x & 63u) * 4u;
+    c.lo = (threadIdx.x & 31u) * 4u;
     c.ek = ek;
     c.fcw = load_blk(ek + 8 + 8 * stop);
     c.outp = out + key * out_stride + local * (16ull << D);
@@ -325,7 +356,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     const uint64_t key = q / pts_per_key;
     const uint32_t* ek = ekeys + key * ((uint64_t)(stop + 2) * 8);
     const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
-    const uint32_t lo = (threadIdx.x & 63u) * 4u;
+    const uint32_t lo = (threadIdx.x & 31u) * 4u;
     const uint64_t x = xs[q];
     Node n;
     n.s = load_blk(ek);

@@ -83,6 +83,14 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: build it with `make -C dpf-go_amd` (no CPU fallback exists)")
+        # One HIP runtime per process: torch ships its own libamdhip64.so
+        # (DT_NEEDED "libamdhip64.so"), ours resolves "libamdhip64.so.7".
+        # Loading torch first makes both bind to torch's copy, so device
+        # pointers and streams handed over from torch are valid here.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

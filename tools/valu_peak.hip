@@ -34,10 +34,22 @@ __global__ __launch_bounds__(256) void k_valu(uint32_t* out, uint32_t seed) {
 #define BOP_(n) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x96" : "+v"(a##n) : "v"(b), "v"(c));
 #define PERM_(n) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(a##n) : "v"(b), "v"(c));
 #define ALIGN_(n) asm volatile("v_alignbit_b32 %0, %0, %0, 8" : "+v"(a##n));
+#define ANDOR_(n) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a##n) : "v"(b), "v"(c));
+#define LSHLOR_(n) asm volatile("v_lshl_or_b32 %0, %0, 8, %1" : "+v"(a##n) : "v"(b));
+#define BFE_(n) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(a##n));
+#define SDWA_(n) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a##n) : "v"(b));
+#define LSHR_(n) asm volatile("v_lshrrev_b32 %0, 8, %0" : "+v"(a##n));
+#define CND_(n) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##n) : "v"(b));
         if constexpr (KIND == 0) { REP8(XOR_) REP8(XOR_) }
         if constexpr (KIND == 1) { REP8(BOP_) REP8(BOP_) }
         if constexpr (KIND == 2) { REP8(PERM_) REP8(PERM_) }
         if constexpr (KIND == 3) { REP8(ALIGN_) REP8(ALIGN_) }
+        if constexpr (KIND == 4) { REP8(ANDOR_) REP8(ANDOR_) }
+        if constexpr (KIND == 5) { REP8(LSHLOR_) REP8(LSHLOR_) }
+        if constexpr (KIND == 6) { REP8(BFE_) REP8(BFE_) }
+        if constexpr (KIND == 7) { REP8(SDWA_) REP8(SDWA_) }
+        if constexpr (KIND == 8) { REP8(LSHR_) REP8(LSHR_) }
+        if constexpr (KIND == 9) { REP8(CND_) REP8(CND_) }
     }
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
@@ -60,6 +72,32 @@ __global__ __launch_bounds__(1024) void k_lds(uint32_t* out, uint32_t seed) {
         for (int j = 0; j < 8; ++j) {
             uint32_t a = __builtin_amdgcn_perm(x[j], lo, 0x0c0c0600u);
             x[j] ^= *(const uint32_t*)((const char*)tab + a);
+        }
+    }
+    uint32_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= x[j];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+__global__ __launch_bounds__(1024) void k_lds64(uint32_t* out, uint32_t seed) {
+    __shared__ uint2 tab[256 * 32];
+    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) tab[i] = make_uint2(i * 0x9e3779b9u, i);
+    __syncthreads();
+    const uint32_t lo = (threadIdx.x & 31) * 8;
+    uint32_t x[8];
+    for (int j = 0; j < 8; ++j) x[j] = (seed + threadIdx.x * 8 + j) * 2654435761u;
+    for (int i = 0; i < kIters; ++i) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t a = __builtin_amdgcn_perm(x[j], lo, 0x0c0c0500u);
+            uint2 v = *(const uint2*)((const char*)tab + a);
+            x[j] ^= v.x + v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t a = __builtin_amdgcn_perm(x[j], lo, 0x0c0c0600u);
+            uint2 v = *(const uint2*)((const char*)tab + a);
+            x[j] ^= v.x + v.y;
         }
     }
     uint32_t r = 0;
@@ -102,11 +140,22 @@ int main() {
     const int lblocks = cus * 2;   // 64 KiB LDS each -> 2 per CU
     double t_lds = time_ms([&] { hipLaunchKernelGGL(k_lds, dim3(lblocks), dim3(1024), 0, 0, out, 1u); });
     const double lds_ops = (double)lblocks * 1024 * kIters * 16;
+    double t_lds64 = time_ms([&] { hipLaunchKernelGGL(k_lds64, dim3(lblocks), dim3(1024), 0, 0, out, 1u); });
+    double t_andor = time_ms([&] { hipLaunchKernelGGL(k_valu<4>, dim3(blocks), dim3(threads), 0, 0, out, 1u); });
+    double t_lshlor = time_ms([&] { hipLaunchKernelGGL(k_valu<5>, dim3(blocks), dim3(threads), 0, 0, out, 1u); });
+    double t_bfe = time_ms([&] { hipLaunchKernelGGL(k_valu<6>, dim3(blocks), dim3(threads), 0, 0, out, 1u); });
+    double t_sdwa = time_ms([&] { hipLaunchKernelGGL(k_valu<7>, dim3(blocks), dim3(threads), 0, 0, out, 1u); });
+    double t_lshr = time_ms([&] { hipLaunchKernelGGL(k_valu<8>, dim3(blocks), dim3(threads), 0, 0, out, 1u); });
+    double t_cnd = time_ms([&] { hipLaunchKernelGGL(k_valu<9>, dim3(blocks), dim3(threads), 0, 0, out, 1u); });
     CHK(hipGetLastError());
     printf("{\"device\": \"%s\", \"cus\": %d, \"clock_mhz\": %d, "
            "\"v_xor_b32_Tops\": %.2f, \"v_bitop3_b32_Tops\": %.2f, \"v_perm_b32_Tops\": %.2f, "
-           "\"v_alignbit_b32_Tops\": %.2f, \"ds_read_b32_lookup_G_per_s\": %.1f}\n",
+           "\"v_alignbit_b32_Tops\": %.2f, \"ds_read_b32_lookup_G_per_s\": %.1f, \"ds_read_b64_lookup_G_per_s\": %.1f, "
+           "\"v_and_or_b32_Tops\": %.2f, \"v_lshl_or_b32_Tops\": %.2f, \"v_bfe_u32_Tops\": %.2f, "
+           "\"v_mov_b32_sdwa_Tops\": %.2f, \"v_lshrrev_b32_Tops\": %.2f, \"v_cndmask_b32_Tops\": %.2f}\n",
            p.gcnArchName, cus, p.clockRate / 1000, lane_ops / t_xor / 1e9, lane_ops / t_bop / 1e9,
-           lane_ops / t_prm / 1e9, lane_ops / t_aln / 1e9, lds_ops / t_lds / 1e6);
+           lane_ops / t_prm / 1e9, lane_ops / t_aln / 1e9, lds_ops / t_lds / 1e6, lds_ops / t_lds64 / 1e6,
+           lane_ops / t_andor / 1e9, lane_ops / t_lshlor / 1e9, lane_ops / t_bfe / 1e9, lane_ops / t_sdwa / 1e9,
+           lane_ops / t_lshr / 1e9, lane_ops / t_cnd / 1e9);
     return 0;
 }
