@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
 """bench.py — DPF evaluation throughput on MI355X (driver contract).
 
-A "step" is one batched EvalFull of BASELINE.json configs[1]: 4096 keys x
-logN=20 (2^32 leaf points, 100,655,104 AES-128-MMO blocks), keys already
-resident in HBM, output left in HBM.  With --gpus N each rank (one process
-per GPU, launched by torch.distributed.run) evaluates its own 4096 keys:
-weak scaling, no collective on the data path; value = points of all ranks /
-max-over-ranks time.
+Default workload (the headline, BASELINE.json configs[1]): a "step" is one
+batched EvalFull of 4096 keys x logN=20 (2^32 leaf points, 100,655,104
+AES-128-MMO blocks) with keys already resident in HBM and the output left in
+HBM.  With --gpus N each rank (one process per GPU, torch.distributed.run)
+evaluates its own 4096 keys: weak scaling, no collective on the data path;
+value = points of all ranks / max-over-ranks time.
 
-Rank 0 prints ONE JSON line with the metric, a "roofline" object for the
-tree kernel (integer VALU bound, timed with HIP events on the launch
-stream), and a "cpu_baseline" object (the oracle's reference-faithful C
-restatement on AES-NI, timed on a bounded sample on this host).
+Rank 0 prints ONE JSON line: the metric, a "roofline" object for the tree
+kernel (integer-VALU bound; its time from HIP events recorded on the launch
+stream around every k_evalfull of the timed steps), and a "cpu_baseline"
+object (the oracle's reference-faithful C restatement on AES-NI, timed on a
+bounded sample on this host).
 
-Other workloads (--workload eval|split|pir) are parity-test / secondary
-measurements, reported on separate lines only when asked for.
+Secondary workloads (--workload), each its own JSON line:
+  eval   configs[2]: 2^16 keys x 2^10 random points, logN=20 per GPU (weak)
+  split  configs[3]: ONE key, logN=32, split by top-level subtree (strong)
+  pir    configs[4]: 2-server PIR answer, logN=24, DB 2^24 x 32 B sharded
+         over the GPUs, B queries (--batch), partials all-gathered + host XOR
 """
 from __future__ import annotations
 
@@ -34,6 +38,7 @@ GATES_PER_AES = 22928          # 2-input gate-equivalents per AES-128-MMO block
 # Override of the measured v_bitop3_b32 rate (Tops), else profiles/r01_valu_peak.json.
 VALU_PEAK_TOPS = float(os.environ.get("DPF_VALU_PEAK_TOPS", "0") or 0) or None
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (spec)
+METRIC = "DPF leaf points/sec (EvalFull logN=20, batched keys) + AES blocks/sec"
 
 
 def stop_of(logN: int) -> int:
@@ -55,6 +60,34 @@ def load_peaks() -> dict:
         d = {}
     return {"bitop3_Tops": float(VALU_PEAK_TOPS or d.get("v_bitop3_b32_Tops", 59.7)),
             "lds_lookups_Gs": float(d.get("ds_read_b32_lookup_G_per_s", 16438.3))}
+
+
+def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float) -> dict:
+    """PRG roofline: 22,928 two-input gate-equivalents per
+    AES-MMO block; ceiling = measured v_bitop3_b32 lane-op rate x 32 bit-lanes
+    x 2 gates per bitop3 (the stricter, bitop3 denominator)."""
+    peaks = load_peaks()
+    achieved = aes_rate * GATES_PER_AES / 1e12
+    peak = peaks["bitop3_Tops"] * 32 * 2
+    gbs = hbm_bytes / (k_ms * 1e-3) / 1e9
+    r = {
+        "bound": "valu",
+        "achieved": round(achieved, 1),
+        "peak": round(peak, 1),
+        "unit": "Tgate/s (2-input gate-equivalents; 22,928 per AES-128-MMO block)",
+        "frac": round(achieved / peak, 4),
+        "traffic": None,
+        "kernel": kernel,
+        "kernel_ms": round(k_ms, 4),
+        "aes_blocks_per_s": aes_rate,
+        "lds_lookup_frac": round(aes_rate * 160 / (peaks["lds_lookups_Gs"] * 1e9), 4),
+        "hbm_GBs": round(gbs, 1),
+        "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+    }
+    tr = os.environ.get("DPF_TRAFFIC_BYTES")
+    if tr:
+        r["traffic"] = float(tr)
+    return r
 
 
 def cpu_baseline(logN: int, target_s: float = 10.0) -> dict:
@@ -86,142 +119,255 @@ def cpu_baseline(logN: int, target_s: float = 10.0) -> dict:
                       f"{cores} threads, AES-NI one block per call; oracle/dpf_oracle.c)"}
 
 
+class Ctx:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        import dpf
+        self.torch, self.dist, self.dpf = torch, dist, dpf
+        self.args = args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world > 1:
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+        self.dev = torch.device("cuda", self.local)
+        torch.cuda.set_device(self.dev)
+        dpf.gpu_init(0)
+        self.stream = torch.cuda.current_stream(self.dev)
+
+    def timed(self, step, steps, warmup):
+        """Warmup, then `steps` steps between barrier+sync pairs; returns the
+        max-over-ranks wall time and the mean kernel time of the event pairs."""
+        torch, dist = self.torch, self.dist
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for _ in range(warmup):
+            step(None)
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(evs[i])
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            dist.barrier()
+        t_wall = time.perf_counter() - t0
+        if self.world > 1:
+            t = torch.tensor([t_wall], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t_wall = float(t.item())
+        k_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+        return t_wall, k_ms
+
+    def line(self, **kw):
+        base = {"n_gpus": self.world, "steps": self.args.steps, "warmup": self.args.warmup,
+                "higher_is_better": True, "vs_baseline": None, "dtype": "u32"}
+        base.update(kw)
+        return base
+
+
+def wl_evalfull(c: Ctx) -> dict:
+    a, dpf, torch = c.args, c.dpf, c.torch
+    from dpf import synth
+    logN, nk = a.logN, a.nkeys
+    kl, olen = dpf.key_len(logN), dpf.evalfull_len(logN)
+    al, s0, s1 = synth.key_seeds(nk, logN, first=c.rank * nk)      # this rank's own keys
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=c.dev)
+    d_out = torch.empty(nk * olen, dtype=torch.uint8, device=c.dev)
+
+    def step(ev):
+        dpf.expand_keys_dev(d_keys, kl, nk, logN, d_work, device=c.local, stream=c.stream)
+        if ev:
+            ev[0].record(c.stream)
+        dpf.evalfull_expanded_dev(d_work, nk, logN, d_out, device=c.local, stream=c.stream)
+        if ev:
+            ev[1].record(c.stream)
+
+    t_wall, k_ms = c.timed(step, a.steps, a.warmup)
+    if a.check and c.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        idx = np.unique(np.linspace(0, nk - 1, 8).astype(int))
+        got = d_out.view(nk, olen)[torch.from_numpy(idx).to(c.dev)].cpu().numpy()
+        assert np.array_equal(got, oracle.evalfull_batch(ka[idx], logN, nthreads=8)), "output differs from oracle"
+    sec = t_wall / a.steps
+    aes = nk * aes_full(logN)
+    line = c.line(metric=METRIC, value=nk * (1 << logN) * c.world / sec, unit="points/s",
+                  ms_per_step=sec * 1e3, scaling="weak",
+                  data="synthetic (SplitMix64 seed 0x5EEDD9F0 keys via host Gen)",
+                  config={"workload": f"batched EvalFull, {nk} keys x logN={logN} per GPU (BASELINE configs[1])",
+                          "keys_per_gpu": nk, "logN": logN, "aes": "lds-ttable",
+                          "parallelism": f"key-shard x{c.world}"},
+                  aes_blocks_per_s=aes * c.world / sec)
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), f"k_evalfull<{min(stop_of(logN), 7)},true>", k_ms,
+                                    nk * olen + nk * (stop_of(logN) + 2) * 32)
+    return line
+
+
+def wl_eval(c: Ctx) -> dict:
+    a, dpf, torch = c.args, c.dpf, c.torch
+    from dpf import synth
+    logN, nk, ppk = a.logN, a.eval_keys, a.eval_points
+    kl = dpf.key_len(logN)
+    al, s0, s1 = synth.key_seeds(nk, logN, first=c.rank * nk)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    xs = synth.eval_points(nk, ppk, logN, master=0x5EEDD9F1 + c.rank)
+    d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
+    d_xs = torch.from_numpy(xs.reshape(-1).view(np.int64)).to(c.dev)
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=c.dev)
+    d_out = torch.empty(nk * ppk, dtype=torch.uint8, device=c.dev)
+
+    def step(ev):
+        if ev:
+            ev[0].record(c.stream)
+        dpf.eval_batch_dev(d_keys, kl, nk, d_xs, ppk, logN, d_out, d_work, device=c.local, stream=c.stream)
+        if ev:
+            ev[1].record(c.stream)
+
+    t_wall, k_ms = c.timed(step, a.steps, a.warmup)
+    if a.check and c.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        got = d_out.view(nk, ppk)[:64].cpu().numpy()
+        assert np.array_equal(got, oracle.eval_batch(ka[:64], xs[:64], logN, nthreads=8)), "Eval differs"
+    sec = t_wall / a.steps
+    q = nk * ppk
+    aes = q * (stop_of(logN) + 1)
+    line = c.line(metric="DPF Eval point queries/sec (batched Eval)", value=q * c.world / sec, unit="queries/s",
+                  ms_per_step=sec * 1e3, scaling="weak", data="synthetic keys + uniform points",
+                  config={"workload": f"batched Eval, {nk} keys x {ppk} points, logN={logN} per GPU "
+                                      f"(BASELINE configs[2])", "logN": logN, "parallelism": f"key-shard x{c.world}"},
+                  aes_blocks_per_s=aes * c.world / sec)
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_eval", k_ms,
+                                    q * 9 + nk * (stop_of(logN) + 2) * 32)
+    return line
+
+
+def wl_split(c: Ctx) -> dict:
+    a, dpf, torch = c.args, c.dpf, c.torch
+    from dpf import synth, shard
+    logN = a.split_logN
+    kl = dpf.key_len(logN)
+    pb, prefix = shard.subtree_split(c.world, c.rank)
+    al, s0, s1 = synth.key_seeds(1, logN, first=777)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)          # the same key on every rank
+    part = dpf.evalfull_len(logN) >> pb
+    d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
+    d_work = torch.empty(dpf.workspace_size(1, logN), dtype=torch.uint8, device=c.dev)
+    d_out = torch.empty(part, dtype=torch.uint8, device=c.dev)
+    dpf.expand_keys_dev(d_keys, kl, 1, logN, d_work, device=c.local, stream=c.stream)
+
+    def step(ev):
+        if ev:
+            ev[0].record(c.stream)
+        dpf.evalfull_expanded_dev(d_work, 1, logN, d_out, prefix_bits=pb, prefix=prefix, device=c.local,
+                                  stream=c.stream)
+        if ev:
+            ev[1].record(c.stream)
+
+    t_wall, k_ms = c.timed(step, a.steps, a.warmup)
+    if a.check and c.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        head = d_out[:16].cpu().numpy()
+        base = prefix << (logN - pb)
+        for q in range(0, 128, 17):
+            assert ((head[q >> 3] >> (q & 7)) & 1) == oracle.eval_(ka[0].tobytes(), base + q, logN, aesni=True)
+    sec = t_wall / a.steps
+    stop = stop_of(logN)
+    aes = 3 * (1 << (stop - pb)) - 2 + pb                    # per rank: subtree + prefix walk
+    line = c.line(metric="DPF leaf points/sec (single-key EvalFull split by subtree)",
+                  value=(1 << logN) / sec, unit="points/s", ms_per_step=sec * 1e3, scaling="strong",
+                  data="synthetic key", config={"workload": f"one key EvalFull logN={logN} split over "
+                                                            f"{c.world} GPU(s) (BASELINE configs[3])",
+                                                "logN": logN, "parallelism": f"subtree-split x{c.world}"},
+                  aes_blocks_per_s=aes * c.world / sec)
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7,false>", k_ms, part)
+    return line
+
+
+def wl_pir(c: Ctx) -> dict:
+    a, dpf, torch = c.args, c.dpf, c.torch
+    from dpf import synth, shard
+    logN, nk = a.pir_logN, a.batch
+    nrec = 1 << logN
+    kl = dpf.key_len(logN)
+    pb, prefix = shard.subtree_split(c.world, c.rank)
+    lo, hi = shard.db_slice(nrec, logN, c.world, c.rank)
+    db = synth.db_bytes(hi * 32)[lo * 32:]                    # this rank's slice of the synthetic DB
+    al, s0, s1 = synth.key_seeds(nk, logN, first=4242)       # the same queries on every server GPU
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
+    d_db = torch.from_numpy(db).to(c.dev)
+    d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=c.dev)
+    d_work = torch.empty(dpf.pir_workspace_size(nk, logN, pb), dtype=torch.uint8, device=c.dev)
+    result = {}
+
+    def step(ev):
+        if ev:
+            ev[0].record(c.stream)
+        dpf.pir_answer_dev(d_keys, kl, nk, logN, d_db, hi - lo, d_ans, d_work, prefix_bits=pb, prefix=prefix,
+                           device=c.local, stream=c.stream)
+        if ev:
+            ev[1].record(c.stream)
+        if c.world > 1:
+            result["ans"] = shard.gather_xor(d_ans.view(nk, 32))
+        else:
+            result["ans"] = d_ans.view(nk, 32).cpu().numpy()
+
+    t_wall, k_ms = c.timed(step, a.steps, a.warmup)
+    if a.check and c.rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        full_db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+        for i in range(min(nk, 4)):
+            want = oracle.pir_answer(ka[i].tobytes(), logN, full_db, 0, nrec)
+            assert result["ans"][i].tobytes() == want, "PIR answer differs from oracle"
+    sec = t_wall / a.steps
+    aes = nk * (3 * (1 << (stop_of(logN) - pb)) - 2)
+    line = c.line(metric="2-server PIR answered queries/sec per server (EvalFull logN=24 + XOR fold)",
+                  value=nk / sec, unit="queries/s", ms_per_step=sec * 1e3, scaling="strong",
+                  data="synthetic DB (SplitMix64) + keys",
+                  config={"workload": f"PIR, DB 2^{logN} x 32 B sharded over {c.world} GPU(s), batch {nk} "
+                                      f"(BASELINE configs[4])", "logN": logN, "batch": nk,
+                          "parallelism": f"db-shard x{c.world} + all_gather/XOR"},
+                  aes_blocks_per_s=aes * c.world / sec)
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_evalfull+k_pir_fold", k_ms,
+                                    (hi - lo) * 32 + nk * ((hi - lo) // 8) * 2)
+    return line
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", choices=["evalfull", "eval", "split", "pir"], default="evalfull")
     ap.add_argument("--logN", type=int, default=20)
     ap.add_argument("--nkeys", type=int, default=4096)
+    ap.add_argument("--eval-keys", type=int, default=1 << 16)
+    ap.add_argument("--eval-points", type=int, default=1 << 10)
+    ap.add_argument("--split-logN", type=int, default=32)
+    ap.add_argument("--pir-logN", type=int, default=24)
+    ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--check", action="store_true", help="verify a sample of outputs against the oracle")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-    import dpf
-    from dpf import synth
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    dpf.gpu_init(0)
-
-    logN, nk = args.logN, args.nkeys
-    kl = dpf.key_len(logN)
-    olen = dpf.evalfull_len(logN)
-    # Each rank its own synthetic keys (keys rank*nk ..), generated on the host.
-    al, s0, s1 = synth.key_seeds(nk, logN, first=rank * nk)
-    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
-    d_keys = torch.from_numpy(ka.reshape(-1)).to(dev)
-    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=dev)
-    d_out = torch.empty(nk * olen, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
-    def step():
-        dpf.expand_keys_dev(d_keys, kl, nk, logN, d_work, device=local, stream=stream)
-        dpf.evalfull_expanded_dev(d_work, nk, logN, d_out, device=local, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t_wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([t_wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_wall = float(t.item())
-
-    # Tree-kernel-only timing with HIP events on the launch stream.
-    dpf.expand_keys_dev(d_keys, kl, nk, logN, d_work, device=local, stream=stream)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    reps = max(3, min(args.steps, 20))
-    ev[0].record(stream)
-    for _ in range(reps):
-        dpf.evalfull_expanded_dev(d_work, nk, logN, d_out, device=local, stream=stream)
-    ev[1].record(stream)
-    torch.cuda.synchronize(dev)
-    k_ms = ev[0].elapsed_time(ev[1]) / reps
-
-    if args.check and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        idx = np.unique(np.linspace(0, nk - 1, 8).astype(int))
-        got = d_out.view(nk, olen)[torch.from_numpy(idx).to(dev)].cpu().numpy()
-        want = oracle.evalfull_batch(ka[idx], logN, nthreads=8)
-        assert np.array_equal(got, want), "bench output differs from oracle"
-
-    pts_per_step = nk * (1 << logN) * world
-    aes_per_step = nk * aes_full(logN) * world
-    ms_per_step = t_wall / args.steps * 1e3
-    value = pts_per_step / (t_wall / args.steps)
-
-    aes_per_launch = nk * aes_full(logN)
-    aes_rate = aes_per_launch / (k_ms * 1e-3)
-    peaks = load_peaks()
-    # PRG roofline: 22,928 two-input gate-equivalents per AES-MMO
-    # block; ceiling = measured v_bitop3_b32 lane-op rate x 32 bit-lanes x 2
-    # gates per bitop3 (the stricter, bitop3 denominator).
-    achieved = aes_rate * GATES_PER_AES / 1e12
-    peak = peaks["bitop3_Tops"] * 32 * 2
-    bytes_per_launch = nk * olen + nk * (stop_of(logN) + 2) * 32
-    roofline = {
-        "bound": "valu",
-        "achieved": round(achieved, 1),
-        "peak": round(peak, 1),
-        "unit": "Tgate/s (2-input gate-equivalents; 22,928 per AES-128-MMO block)",
-        "frac": round(achieved / peak, 4),
-        "traffic": None,
-        "kernel": f"k_evalfull<{min(stop_of(logN), 7)},true>",
-        "kernel_ms": round(k_ms, 4),
-        "aes_blocks_per_s": aes_rate,
-        "lds_lookup_frac": round(aes_rate * 160 / (peaks["lds_lookups_Gs"] * 1e9), 4),
-        "hbm_write_GBs": round(bytes_per_launch / (k_ms * 1e-3) / 1e9, 1),
-        "hbm_frac": round(bytes_per_launch / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-    }
-    tr_env = os.environ.get("DPF_TRAFFIC_BYTES")
-    if tr_env:
-        roofline["traffic"] = float(tr_env)
-
-    if rank == 0:
-        line = {
-            "metric": "DPF leaf points/sec (EvalFull logN=20, batched keys) + AES blocks/sec",
-            "value": value,
-            "unit": "points/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (SplitMix64 seed 0x5EEDD9F0 keys via host Gen)",
-            "config": {"workload": f"batched EvalFull, {nk} keys x logN={logN} per GPU (BASELINE configs[1])",
-                       "keys_per_gpu": nk, "logN": logN, "aes": "lds-ttable",
-                       "parallelism": f"key-shard x{world}"},
-            "aes_blocks_per_s": aes_per_step / (t_wall / args.steps),
-            "roofline": roofline,
-        }
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(logN, args.cpu_seconds)
+    c = Ctx(args)
+    line = {"evalfull": wl_evalfull, "eval": wl_eval, "split": wl_split, "pir": wl_pir}[args.workload](c)
+    if c.rank == 0:
+        if args.workload == "evalfull" and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.logN, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if c.world > 1:
+        c.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -19,6 +19,7 @@
 #include "../../include/dpf_hip.h"
 #include "dpf_internal.hpp"
 #include "dpf_kernels.hpp"
+#include "pir_kernels.hpp"
 
 using dpfh::full_len;
 using dpfh::key_len;
@@ -219,6 +220,11 @@ int pick_ngpus(int ngpus) {
     return ngpus <= 0 ? have : std::min(ngpus, have);
 }
 
+// Expanded keys at the start of a PIR workspace, padded to 256 B.
+size_t pir_ek_bytes(size_t nkeys, uint32_t logN) {
+    return (nkeys * dpfk::ek_words(stop_of(logN)) * 4 + 255) & ~(size_t)255;
+}
+
 }  // namespace
 
 extern "C" {
@@ -376,6 +382,120 @@ int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint
     HIP_TRY(dpfk::launch_evalfull((const uint32_t*)d_work, nkeys, stop, prefix_bits, prefix, d_out, stride,
                                   (hipStream_t)stream));
     return DPF_OK;
+}
+
+// ------------------------------------------------------------------ PIR ---
+
+size_t dpf_pir_workspace_size(size_t nkeys, uint32_t logN, uint32_t prefix_bits) {
+    const uint32_t stop = stop_of(logN);
+    const uint32_t pb = prefix_bits > stop ? stop : prefix_bits;
+    return pir_ek_bytes(nkeys, logN) + nkeys * ((size_t)16 << (stop - pb));
+}
+
+int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN,
+                       uint32_t prefix_bits, uint64_t prefix, const uint8_t* d_db, uint64_t nrec, uint8_t* d_ans,
+                       void* d_work, void* stream) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const uint32_t stop = stop_of(logN);
+    if (prefix_bits > stop || (prefix >> prefix_bits) != 0) return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
+    const uint64_t slice = logN - prefix_bits >= 64 ? ~0ull : (1ull << (logN - prefix_bits));
+    if (nrec > slice) return fail(DPF_ERR_PARAM, "dpf: more DB records than the subtree's domain");
+    DeviceGuard g(device);
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(d_ans, 0, nkeys * 32, st));
+    if (nkeys == 0 || nrec == 0) return DPF_OK;
+    uint32_t* ek = (uint32_t*)d_work;
+    uint8_t* bits = (uint8_t*)d_work + pir_ek_bytes(nkeys, logN);
+    const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
+    int rc = enqueue_full(d_keys, klen, nkeys, logN, prefix_bits, prefix, bits, ek, st);
+    if (rc) return rc;
+    HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, (uint32_t)nkeys, (uint32_t*)d_ans,
+                                  st));
+    return DPF_OK;
+}
+
+struct PirDb {
+    uint32_t logN = 0, pbits = 0;
+    uint64_t nrec = 0;
+    std::vector<void*> shard;      // per device: its DB slice
+    std::vector<uint64_t> shard_n; // records in that slice
+};
+
+int dpf_pir_db_create(const uint8_t* db, uint64_t nrec, uint32_t logN, int ngpus, void** handle) {
+    if (!handle) return fail(DPF_ERR_PARAM, "dpf: null handle");
+    *handle = nullptr;
+    if (logN > 63 || (logN < 64 && nrec > (1ull << logN))) return fail(DPF_ERR_PARAM, "dpf: DB larger than 2^logN");
+    const int have = pick_ngpus(ngpus);
+    if (have <= 0) return have;
+    const int want = ngpus <= 0 ? have : ngpus;
+    uint32_t pb = 0;
+    while ((1 << pb) < want) ++pb;
+    if ((1 << pb) != want || want > have || pb > stop_of(logN))
+        return fail(DPF_ERR_PARAM, "dpf: ngpus must be a power of two <= opened devices and 2^(logN-7)");
+    auto h = std::make_unique<PirDb>();
+    h->logN = logN;
+    h->pbits = pb;
+    h->nrec = nrec;
+    const uint64_t slice = 1ull << (logN - pb);
+    for (int g = 0; g < want; ++g) {
+        const uint64_t lo = std::min<uint64_t>(nrec, (uint64_t)g * slice);
+        const uint64_t hi = std::min<uint64_t>(nrec, lo + slice);
+        DeviceGuard gd(g_devs[(size_t)g]->id);
+        void* p = nullptr;
+        const size_t bytes = std::max<uint64_t>(hi - lo, 1) * 32;
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            for (void* q : h->shard) (void)hipFree(q);
+            return fail(DPF_ERR_NOMEM, "dpf: DB shard allocation failed");
+        }
+        if (hi > lo && hipMemcpy(p, db + lo * 32, (hi - lo) * 32, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(p);
+            for (void* q : h->shard) (void)hipFree(q);
+            return fail(DPF_ERR_HIP, "dpf: DB upload failed");
+        }
+        h->shard.push_back(p);
+        h->shard_n.push_back(hi - lo);
+    }
+    *handle = h.release();
+    return DPF_OK;
+}
+
+int dpf_pir_answer(void* handle, const uint8_t* keys, size_t klen, size_t nkeys, uint8_t* ans) {
+    PirDb* h = (PirDb*)handle;
+    if (!h) return fail(DPF_ERR_PARAM, "dpf: null PIR handle");
+    if (int rc = check_key(klen, h->logN)) return rc;
+    const int g = (int)h->shard.size();
+    std::vector<std::vector<uint8_t>> part((size_t)g, std::vector<uint8_t>(nkeys * 32));
+    int rc = shard((size_t)g, g, [&](int dev, size_t lo, size_t hi) {
+        (void)hi;
+        Dev& d = *g_devs[(size_t)dev];
+        std::lock_guard<std::mutex> lk(d.mu);
+        DeviceGuard gd(d.id);
+        HIP_TRY(hipError_t(d.keys.ensure(std::max<size_t>(1, nkeys * klen))));
+        HIP_TRY(hipError_t(d.work.ensure(dpf_pir_workspace_size(nkeys, h->logN, h->pbits))));
+        HIP_TRY(hipError_t(d.out.ensure(std::max<size_t>(32, nkeys * 32))));
+        HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nkeys * klen, hipMemcpyHostToDevice, d.st));
+        int r = dpf_pir_answer_dev(d.id, (const uint8_t*)d.keys.p, klen, nkeys, h->logN, h->pbits, lo,
+                                   (const uint8_t*)h->shard[lo], h->shard_n[lo], (uint8_t*)d.out.p, d.work.p, d.st);
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(part[lo].data(), d.out.p, nkeys * 32, hipMemcpyDeviceToHost, d.st));
+        HIP_TRY(hipStreamSynchronize(d.st));
+        return DPF_OK;
+    });
+    if (rc) return rc;
+    memset(ans, 0, nkeys * 32);
+    for (int i = 0; i < g; ++i)
+        for (size_t b = 0; b < nkeys * 32; ++b) ans[b] ^= part[(size_t)i][b];
+    return DPF_OK;
+}
+
+void dpf_pir_db_free(void* handle) {
+    PirDb* h = (PirDb*)handle;
+    if (!h) return;
+    for (size_t i = 0; i < h->shard.size(); ++i) {
+        DeviceGuard gd(g_devs[i]->id);
+        (void)hipFree(h->shard[i]);
+    }
+    delete h;
 }
 
 }  // extern "C"

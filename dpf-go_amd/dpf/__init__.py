@@ -72,6 +72,11 @@ SIGNATURES = {
     "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _vp]),
     "dpf_expand_keys_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp]),
     "dpf_evalfull_expanded_dev": (_int, [_int, _vp, _sz, _u32, _u32, _u64, _vp, _vp]),
+    "dpf_pir_workspace_size": (_sz, [_sz, _u32, _u32]),
+    "dpf_pir_answer_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _u64, _vp, _vp, _vp]),
+    "dpf_pir_db_create": (_int, [_u8p, _u64, _u32, _int, ctypes.POINTER(_vp)]),
+    "dpf_pir_answer": (_int, [_vp, _u8p, _sz, _sz, _u8p]),
+    "dpf_pir_db_free": (None, [_vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -258,3 +263,49 @@ def evalfull_expanded_dev(d_work, nkeys: int, logN: int, d_out, prefix_bits: int
                           device: int = 0, stream=None) -> None:
     _check(lib().dpf_evalfull_expanded_dev(device, _ptr(d_work), nkeys, logN, prefix_bits, prefix, _ptr(d_out),
                                            _stream_handle(stream)))
+
+
+# ------------------------------------------------------------------ PIR ---
+def pir_workspace_size(nkeys: int, logN: int, prefix_bits: int = 0) -> int:
+    return int(lib().dpf_pir_workspace_size(nkeys, logN, prefix_bits))
+
+
+def pir_answer_dev(d_keys, key_len_: int, nkeys: int, logN: int, d_db, nrec: int, d_ans, d_work,
+                   prefix_bits: int = 0, prefix: int = 0, device: int = 0, stream=None) -> None:
+    """Server answers (nkeys x 32 B) for the DB slice of subtree (prefix_bits, prefix)."""
+    _check(lib().dpf_pir_answer_dev(device, _ptr(d_keys), key_len_, nkeys, logN, prefix_bits, prefix, _ptr(d_db),
+                                    nrec, _ptr(d_ans), _ptr(d_work), _stream_handle(stream)))
+
+
+class PirDB:
+    """A 32-byte-record DB resident in HBM, sharded by top-level subtree over
+    ngpus GPUs; answer() returns each key's XOR-inner-product (host XOR of
+    the per-GPU partials)."""
+
+    def __init__(self, db: np.ndarray, logN: int, ngpus: int = 1):
+        d = np.ascontiguousarray(db, dtype=np.uint8).reshape(-1)
+        if d.size % 32:
+            raise ValueError("DB size must be a multiple of 32 bytes")
+        self.logN = logN
+        self.nrec = d.size // 32
+        h = _vp()
+        _check(lib().dpf_pir_db_create(_buf(d), self.nrec, logN, ngpus, ctypes.byref(h)))
+        self._h = h
+
+    def answer(self, keys: np.ndarray) -> np.ndarray:
+        kk = np.ascontiguousarray(keys, dtype=np.uint8)
+        n, kl = kk.shape
+        ans = np.zeros((n, 32), np.uint8)
+        _check(lib().dpf_pir_answer(self._h, _buf(kk), kl, n, _buf(ans)))
+        return ans
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().dpf_pir_db_free(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

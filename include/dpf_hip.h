@@ -106,6 +106,28 @@ int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t key_len, size_
 int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
                               uint64_t prefix, uint8_t* d_out, void* stream);
 
+/* ---- 2-server PIR over a DPF (BASELINE configs[4]; no reference
+ *      counterpart: a consumer of EvalFull, SURVEY 8a last row) -----------
+ * Server answer for key k: XOR of the 32-byte records DB[i] with
+ * bit i of EvalFull(key_k, logN) set.  The DB holds nrec <= 2^logN records
+ * of 32 bytes; the two servers' answers XOR to DB[alpha]. */
+
+/* Device form on one GPU: DB slice = records of subtree (prefix_bits,
+ * prefix), i.e. global records [prefix*2^(logN-prefix_bits), ...), d_db
+ * holding nrec <= 2^(logN-prefix_bits) of them.  d_ans = nkeys*32 bytes
+ * (overwritten); d_work = dpf_pir_workspace_size(nkeys, logN, prefix_bits). */
+size_t dpf_pir_workspace_size(size_t nkeys, uint32_t logN, uint32_t prefix_bits);
+int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, uint32_t logN,
+                       uint32_t prefix_bits, uint64_t prefix, const uint8_t* d_db, uint64_t nrec, uint8_t* d_ans,
+                       void* d_work, void* stream);
+
+/* Host form: the DB is uploaded once, sharded by top-level subtree over
+ * ngpus devices (a power of two), each GPU folds its slice and the host
+ * XORs the per-GPU partial answers (RCCL has no XOR reduction). */
+int dpf_pir_db_create(const uint8_t* db, uint64_t nrec, uint32_t logN, int ngpus, void** handle);
+int dpf_pir_answer(void* handle, const uint8_t* keys, size_t key_len, size_t nkeys, uint8_t* ans);
+void dpf_pir_db_free(void* handle);
+
 #ifdef __cplusplus
 }
 #endif
