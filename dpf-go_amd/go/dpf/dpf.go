@@ -1,0 +1,122 @@
+// Package dpf is the MI355X-backed drop-in for the evaluation path of
+// github.com/dkales/dpf-go/dpf: the same exported API (DPFkey, Gen, Eval,
+// EvalFull — reference dpf/dpf.go:7,71,171,243) over the C ABI of
+// libdpf_hip.so (include/dpf_hip.h).  Gen stays on the host (AES-NI);
+// Eval and EvalFull run as gfx950 kernels.  Where the reference panics,
+// this package panics too.
+//
+// Build: make -C dpf-go_amd (produces dpf-go_amd/lib/libdpf_hip.so), then
+// `go test ./...` in this directory on a machine with a gfx950 GPU.
+package dpf
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../lib -ldpf_hip -Wl,-rpath,${SRCDIR}/../../lib
+#include <stdint.h>
+#include "dpf_hip.h"
+*/
+import "C"
+
+import (
+	"crypto/rand"
+	"unsafe"
+)
+
+// DPFkey is one party's key share, byte layout identical to the reference
+// (dpf/dpf.go:89-167): seed[16] | t | per level (sCW[16] | tLCW | tRCW) | finalCW[16].
+type DPFkey []byte
+
+func check(rc C.int) {
+	if rc != 0 {
+		panic("dpf: " + C.GoString(C.dpf_last_error()))
+	}
+}
+
+func u8(b []byte) *C.uint8_t {
+	if len(b) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(unsafe.Pointer(&b[0]))
+}
+
+// Gen mirrors dpf/dpf.go:71: two shares of the point function at alpha
+// over a domain of 2^logN points; seeds come from crypto/rand (:80-81).
+func Gen(alpha uint64, logN uint64) (DPFkey, DPFkey) {
+	if alpha >= (1<<logN) || logN > 63 {
+		panic("dpf: invalid parameters")
+	}
+	var seeds [32]byte
+	if _, err := rand.Read(seeds[:]); err != nil {
+		panic("dpf: crypto/rand failed")
+	}
+	n := int(C.dpf_key_len(C.uint32_t(logN)))
+	ka := make(DPFkey, n)
+	kb := make(DPFkey, n)
+	check(C.dpf_gen_seeded(C.uint64_t(alpha), C.uint32_t(logN), u8(seeds[:16]), u8(seeds[16:]), u8(ka), u8(kb)))
+	return ka, kb
+}
+
+// Eval mirrors dpf/dpf.go:171: this share's bit of f_alpha(x).
+func Eval(k DPFkey, x uint64, logN uint64) byte {
+	var out [1]byte
+	check(C.dpf_eval(u8(k), C.size_t(len(k)), C.uint64_t(x), C.uint32_t(logN), u8(out[:])))
+	return out[0]
+}
+
+// EvalFull mirrors dpf/dpf.go:243: this share of f_alpha over the whole
+// domain, point x at bit x%8 of byte x/8 (16 bytes when logN < 7).
+func EvalFull(key DPFkey, logN uint64) []byte {
+	out := make([]byte, int(C.dpf_evalfull_len(C.uint32_t(logN))))
+	check(C.dpf_evalfull(u8(key), C.size_t(len(key)), C.uint32_t(logN), u8(out)))
+	return out
+}
+
+// EvalFullBatch evaluates many keys of one logN at once, sharded over
+// ngpus GPUs (0 = all); out[i] is EvalFull(keys[i], logN).
+func EvalFullBatch(keys []DPFkey, logN uint64, ngpus int) [][]byte {
+	if len(keys) == 0 {
+		return nil
+	}
+	kl := len(keys[0])
+	packed := make([]byte, kl*len(keys))
+	for i, k := range keys {
+		if len(k) != kl {
+			panic("dpf: keys of different lengths in one batch")
+		}
+		copy(packed[i*kl:], k)
+	}
+	ol := int(C.dpf_evalfull_len(C.uint32_t(logN)))
+	flat := make([]byte, ol*len(keys))
+	check(C.dpf_evalfull_batch(u8(packed), C.size_t(kl), C.size_t(len(keys)), C.uint32_t(logN), u8(flat),
+		C.int(ngpus)))
+	out := make([][]byte, len(keys))
+	for i := range out {
+		out[i] = flat[i*ol : (i+1)*ol : (i+1)*ol]
+	}
+	return out
+}
+
+// EvalBatch answers len(xs[i]) point queries for each key i.
+func EvalBatch(keys []DPFkey, xs [][]uint64, logN uint64, ngpus int) [][]byte {
+	if len(keys) == 0 {
+		return nil
+	}
+	kl, ppk := len(keys[0]), len(xs[0])
+	packed := make([]byte, kl*len(keys))
+	pts := make([]uint64, ppk*len(keys))
+	for i, k := range keys {
+		if len(k) != kl || len(xs[i]) != ppk {
+			panic("dpf: ragged batch")
+		}
+		copy(packed[i*kl:], k)
+		copy(pts[i*ppk:], xs[i])
+	}
+	flat := make([]byte, ppk*len(keys))
+	check(C.dpf_eval_batch(u8(packed), C.size_t(kl), C.size_t(len(keys)),
+		(*C.uint64_t)(unsafe.Pointer(&pts[0])), C.size_t(ppk), C.uint32_t(logN), u8(flat), C.int(ngpus)))
+	out := make([][]byte, len(keys))
+	for i := range out {
+		out[i] = flat[i*ppk : (i+1)*ppk : (i+1)*ppk]
+	}
+	return out
+}
