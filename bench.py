@@ -253,7 +253,8 @@ def wl_split(c: Ctx) -> dict:
     from dpf import synth, shard
     logN = a.split_logN
     kl = dpf.key_len(logN)
-    pb, prefix = shard.subtree_split(c.world, c.rank)
+    W = c.world if c.world > 1 else max(1, a.emulate_world)
+    pb, prefix = shard.subtree_split(W, c.rank)
     al, s0, s1 = synth.key_seeds(1, logN, first=777)
     ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)          # the same key on every rank
     part = dpf.evalfull_len(logN) >> pb
@@ -282,9 +283,11 @@ def wl_split(c: Ctx) -> dict:
     stop = stop_of(logN)
     aes = 3 * (1 << (stop - pb)) - 2 + pb                    # per rank: subtree + prefix walk
     line = c.line(metric="DPF leaf points/sec (single-key EvalFull split by subtree)",
-                  value=(1 << logN) / sec, unit="points/s", ms_per_step=sec * 1e3, scaling="strong",
-                  data="synthetic key", config={"workload": f"one key EvalFull logN={logN} split over "
-                                                            f"{c.world} GPU(s) (BASELINE configs[3])",
+                  value=(1 << logN) / sec, unit="points/s", ms_per_step=sec * 1e3,
+                  scaling="strong", data="synthetic key",
+                  config={"workload": f"one key EvalFull logN={logN} split over {W} GPU(s)"
+                                      + (" (rank 0's share timed on 1 GPU)" if W != c.world else "")
+                                      + " (BASELINE configs[3])",
                                                 "logN": logN, "parallelism": f"subtree-split x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
     line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7,false>", k_ms, part)
@@ -297,8 +300,9 @@ def wl_pir(c: Ctx) -> dict:
     logN, nk = a.pir_logN, a.batch
     nrec = 1 << logN
     kl = dpf.key_len(logN)
-    pb, prefix = shard.subtree_split(c.world, c.rank)
-    lo, hi = shard.db_slice(nrec, logN, c.world, c.rank)
+    W = c.world if c.world > 1 else max(1, a.emulate_world)
+    pb, prefix = shard.subtree_split(W, c.rank)
+    lo, hi = shard.db_slice(nrec, logN, W, c.rank)
     db = synth.db_bytes(hi * 32)[lo * 32:]                    # this rank's slice of the synthetic DB
     al, s0, s1 = synth.key_seeds(nk, logN, first=4242)       # the same queries on every server GPU
     ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
@@ -321,7 +325,7 @@ def wl_pir(c: Ctx) -> dict:
             result["ans"] = d_ans.view(nk, 32).cpu().numpy()
 
     t_wall, k_ms = c.timed(step, a.steps, a.warmup)
-    if a.check and c.rank == 0:
+    if a.check and c.rank == 0 and W == c.world:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         full_db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
@@ -333,8 +337,9 @@ def wl_pir(c: Ctx) -> dict:
     line = c.line(metric="2-server PIR answered queries/sec per server (EvalFull logN=24 + XOR fold)",
                   value=nk / sec, unit="queries/s", ms_per_step=sec * 1e3, scaling="strong",
                   data="synthetic DB (SplitMix64) + keys",
-                  config={"workload": f"PIR, DB 2^{logN} x 32 B sharded over {c.world} GPU(s), batch {nk} "
-                                      f"(BASELINE configs[4])", "logN": logN, "batch": nk,
+                  config={"workload": f"PIR, DB 2^{logN} x 32 B sharded over {W} GPU(s), batch {nk}"
+                                      + (" (rank 0's share timed on 1 GPU)" if W != c.world else "")
+                                      + " (BASELINE configs[4])", "logN": logN, "batch": nk,
                           "parallelism": f"db-shard x{c.world} + all_gather/XOR"},
                   aes_blocks_per_s=aes * c.world / sec)
     line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_evalfull+k_pir_fold", k_ms,
@@ -355,6 +360,8 @@ def main() -> None:
     ap.add_argument("--split-logN", type=int, default=32)
     ap.add_argument("--pir-logN", type=int, default=24)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="split/pir on 1 GPU: time rank 0's share of a W-way split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--check", action="store_true", help="verify a sample of outputs against the oracle")

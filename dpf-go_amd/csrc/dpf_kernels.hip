@@ -11,6 +11,7 @@
 // ascending order exactly like evalFullRecursive's cursor (dpf.go:213-241).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "aes_consts.hpp"
 #include "aes_ttable.hpp"
 #include "dpf_kernels.hpp"
@@ -213,6 +214,80 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     out[q] = (uint8_t)((w >> (b & 31)) & 1u);
 }
 
+// Batched Eval with a shared frontier: many random points of
+// one key share the top of the tree, so a workgroup first expands its key
+// breadth-first to level L (2^L nodes in LDS, 2^L - 2 AES in all instead of
+// L per query), then every query continues from its level-L node: stop - L
+// path AES + the leaf MMO.  At configs[2] (1024 points, logN=20, L=9) that
+// is 1022 + 1024*5 AES per key instead of 1024*14.  Each workgroup loops
+// over keys so the LDS table is filled once.
+template <int L>
+__global__ __launch_bounds__(kBlock, 4) void k_eval_frontier(const uint32_t* __restrict__ ekeys, uint32_t stop,
+                                                             uint32_t logN, const uint64_t* __restrict__ xs,
+                                                             uint64_t nkeys, uint64_t pts_per_key,
+                                                             uint8_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+    // Levels alternate between two node buffers, level L always in A.
+    __shared__ uint4 s_a[1 << L];
+    __shared__ uint32_t s_at[1 << L];
+    __shared__ uint4 s_b[(1 << L) / 2 > 0 ? (1 << L) / 2 : 1];
+    __shared__ uint32_t s_bt[(1 << L) / 2 > 0 ? (1 << L) / 2 : 1];
+    fill_table(s_tab);
+    const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
+    const uint32_t lo = (threadIdx.x & 31u) * 4u;
+    for (uint64_t key = blockIdx.x; key < nkeys; key += gridDim.x) {
+        const uint32_t* ek = ekeys + key * ((uint64_t)(stop + 2) * 8);
+        __syncthreads();   // previous key's queries are done with s_a
+        if (threadIdx.x == 0) {
+            Blk r = load_blk(ek);
+            ((L & 1) ? s_b : s_a)[0] = make_uint4(r.c0, r.c1, r.c2, r.c3);
+            ((L & 1) ? s_bt : s_at)[0] = ek[4];
+        }
+        // breadth-first: level d from level d-1 (d = 1..L)
+        for (int d = 1; d <= L; ++d) {
+            __syncthreads();
+            const bool to_a = ((L - d) & 1) == 0;
+            const uint4* src = to_a ? s_b : s_a;
+            const uint32_t* srct = to_a ? s_bt : s_at;
+            uint4* dst = to_a ? s_a : s_b;
+            uint32_t* dstt = to_a ? s_at : s_bt;
+            const CW cw = load_cw(ek, d - 1);
+            for (uint32_t i = threadIdx.x; i < (1u << (d - 1)); i += blockDim.x) {
+                Node n;
+                const uint4 v = src[i];
+                n.s = {v.x, v.y, v.z, v.w};
+                n.t = srct[i];
+                Node Lc, Rc;
+                expand(tab, lo, n, cw, Lc, Rc);
+                dst[2 * i] = make_uint4(Lc.s.c0, Lc.s.c1, Lc.s.c2, Lc.s.c3);
+                dst[2 * i + 1] = make_uint4(Rc.s.c0, Rc.s.c1, Rc.s.c2, Rc.s.c3);
+                dstt[2 * i] = Lc.t;
+                dstt[2 * i + 1] = Rc.t;
+            }
+        }
+        __syncthreads();
+        const Blk fcw = load_blk(ek + 8 + 8 * stop);
+        for (uint64_t q = threadIdx.x; q < pts_per_key; q += blockDim.x) {
+            const uint64_t gq = key * pts_per_key + q;
+            const uint64_t x = xs[gq];
+            const uint32_t top = (uint32_t)(x >> (logN - L)) & ((1u << L) - 1);
+            Node n;
+            const uint4 v = s_a[top];
+            n.s = {v.x, v.y, v.z, v.w};
+            n.t = s_at[top];
+            for (uint32_t i = L; i < stop; ++i) {
+                CW cw = load_cw(ek, i);
+                walk_step(tab, lo, n, cw, (uint32_t)(x >> (logN - 1 - i)) & 1u);
+            }
+            Blk o = mmo1(tab, lo, KeyFixed<false>{}, n.s);
+            o = leaf_fix(o, n.t, fcw);
+            const uint32_t b = (uint32_t)(x & 127);
+            const uint32_t w = (b >> 5) == 0 ? o.c0 : (b >> 5) == 1 ? o.c1 : (b >> 5) == 2 ? o.c2 : o.c3;
+            out[gq] = (uint8_t)((w >> (b & 31)) & 1u);
+        }
+    }
+}
+
 // ------------------------------------------------------------ launchers ---
 
 hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ek,
@@ -238,10 +313,32 @@ static hipError_t launch_full_d(const uint32_t* ek, uint32_t stop, uint64_t nuni
     return hipGetLastError();
 }
 
+// Per-thread subtree depth.  Deeper subtrees amortise the root-to-subtree
+// walk (ltop AES per thread against 3*2^D - 2), but a small batch of keys
+// then launches too few threads to fill the GPU; shrink D (not below kMinD)
+// until the grid reaches two 512-thread workgroups per CU.
+// DPF_SUBTREE_DEPTH overrides the choice (measurement only).
+static uint32_t pick_depth(uint32_t span, uint64_t nkeys) {
+    static const int forced = [] {
+        const char* e = getenv("DPF_SUBTREE_DEPTH");
+        return e ? atoi(e) : -1;
+    }();
+    uint32_t d = span < kMaxD ? span : kMaxD;
+    if (forced >= 0) return span < (uint32_t)forced ? span : (uint32_t)forced;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const uint64_t fill = (uint64_t)cus * 2 * kBlock;
+    auto threads = [&](uint32_t dd) { return span - dd >= 40 ? ~0ull : nkeys << (span - dd); };
+    while (d > kMinD && threads(d) < fill) --d;
+    return d;
+}
+
 hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
                            uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st) {
     const uint32_t span = stop - prefix_bits;          // levels below the prefix node
-    const uint32_t d = span < kMaxD ? span : kMaxD;     // per-thread subtree depth
+    const uint32_t d = pick_depth(span, nkeys);         // per-thread subtree depth
     const uint32_t ltop = stop - d;                     // levels walked per thread
     const uint32_t units_log = ltop - prefix_bits;      // threads per key = 2^units_log
     const uint64_t nunits = nkeys << units_log;
@@ -259,9 +356,35 @@ hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, ui
     }
 }
 
+template <int L>
+static hipError_t launch_frontier(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs,
+                                  uint64_t nkeys, uint64_t ppk, uint8_t* out, hipStream_t st) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const uint64_t grid = nkeys < (uint64_t)cus * 2 ? nkeys : (uint64_t)cus * 2;
+    hipLaunchKernelGGL((k_eval_frontier<L>), dim3((uint32_t)grid), dim3(kBlock), 0, st, ek, stop, logN, xs, nkeys,
+                       ppk, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
                        uint64_t pts_per_key, uint8_t* out, hipStream_t st) {
     if (nq == 0) return hipSuccess;
+    // Shared frontier at level L when a key's points cover it: 2^L <= ppk / 2.
+    static const bool no_frontier = getenv("DPF_EVAL_NO_FRONTIER") != nullptr;
+    uint32_t L = 0;
+    while (L < kMaxFrontier && L < stop && (2ull << (L + 1)) <= pts_per_key) ++L;
+    if (!no_frontier && L >= 6) {
+        const uint64_t nkeys = nq / pts_per_key;
+        switch (L) {
+            case 6: return launch_frontier<6>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
+            case 7: return launch_frontier<7>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
+            case 8: return launch_frontier<8>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
+            default: return launch_frontier<9>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
+        }
+    }
     const uint64_t blocks = (nq + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_eval, dim3((uint32_t)blocks), dim3(kBlock), 0, st, ek, stop, logN, xs, nq, pts_per_key,
                        out);

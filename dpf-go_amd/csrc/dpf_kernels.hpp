@@ -7,6 +7,8 @@ namespace dpfk {
 
 constexpr int kBlock = 512;    // threads per workgroup (8 waves); 2 workgroups per CU (64 KiB LDS table each)
 constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
+constexpr uint32_t kMinD = 5;  // smallest depth chosen to fill the GPU (walk overhead <= ~13%)
+constexpr uint32_t kMaxFrontier = 9;  // batched Eval: deepest shared level kept in LDS (512 nodes)
 
 // Expanded-key words per key: (stop + 2) records of 8 u32.
 inline uint64_t ek_words(uint32_t stop) { return ((uint64_t)stop + 2) * 8; }

@@ -73,9 +73,21 @@ __global__ __launch_bounds__(64 * kFoldWaves) void k_pir_fold(const uint32_t* __
                                                               uint64_t words_per_key,
                                                               const uint4* __restrict__ db, uint64_t nrec,
                                                               uint32_t nkeys, uint32_t* __restrict__ ans) {
+    constexpr int kWordsPerWave = 64 * kFoldR / 32;
+    constexpr int kWordsPerBlock = kFoldWaves * kWordsPerWave;
     __shared__ uint32_t s_part[kFoldWaves][kFoldMaxB][8];
+    __shared__ uint32_t s_bits[kFoldMaxB][kWordsPerBlock];
     const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t chunk = ((uint64_t)blockIdx.x * kFoldWaves + w) * (64 * kFoldR);
+    // Every key's selection words for this workgroup's records, one
+    // coalesced pass (64 words = 256 B per key), into LDS.
+    {
+        const uint64_t wb = (uint64_t)blockIdx.x * kWordsPerBlock;
+        for (uint32_t i = threadIdx.x; i < nkeys * kWordsPerBlock; i += blockDim.x) {
+            const uint32_t k = i / kWordsPerBlock, o = i % kWordsPerBlock;
+            s_bits[k][o] = wb + o < words_per_key ? bits[k * words_per_key + wb + o] : 0u;
+        }
+    }
     uint32_t rec[kFoldR][8];
 #pragma unroll
     for (int j = 0; j < kFoldR; ++j) {
@@ -89,15 +101,14 @@ __global__ __launch_bounds__(64 * kFoldWaves) void k_pir_fold(const uint32_t* __
             for (int i = 0; i < 8; ++i) rec[j][i] = 0;
         }
     }
+    __syncthreads();
     const uint32_t sh = 31 - (l & 31);
-    const uint64_t wbase = (chunk >> 5) + (l >> 5);
+    const int wbase = w * kWordsPerWave + (l >> 5);
     for (uint32_t k = 0; k < nkeys; ++k) {
-        const uint32_t* bk = bits + k * words_per_key;
         uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < kFoldR; ++j) {
-            const uint64_t wi = wbase + 2 * j;
-            const uint32_t word = wi < words_per_key ? bk[wi] : 0u;
+            const uint32_t word = s_bits[k][wbase + 2 * j];
             const uint32_t m = (uint32_t)((int32_t)(word << sh) >> 31);   // -(bit l of the word)
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[i] = xorsel(acc[i], rec[j][i], m);

@@ -213,3 +213,17 @@ def test_logN32_single_key_property():
     first = d_out[:64].cpu().numpy()
     for q in (0, 1, 200, 511):
         assert ((first[q >> 3] >> (q & 7)) & 1) == oracle.eval_(ka, q, logN, aesni=True)
+
+
+@pytest.mark.parametrize("logN,nk,ppk", [(13, 8, 256), (14, 5, 1000), (20, 6, 1024), (20, 3, 3000), (32, 4, 512),
+                                         (63, 2, 700)])
+def test_eval_frontier_path_vs_oracle(logN, nk, ppk):
+    """Shared-frontier Eval kernel (taken when a key has >= 256 points)."""
+    _, ka, _ = _keys(nk, logN, first=8000 + logN + ppk)
+    xs = synth.eval_points(nk, ppk, logN)
+    xs[:, 0] = 0
+    xs[:, 1] = (1 << logN) - 1
+    xs[:, 2] = xs[:, 3]          # duplicate points
+    got = dpf.eval_batch(ka, xs, logN, ngpus=1)
+    want = oracle.eval_batch(ka, xs, logN, nthreads=NT)
+    assert np.array_equal(got, want)
