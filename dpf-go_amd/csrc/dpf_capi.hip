@@ -174,6 +174,9 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
     return DPF_OK;
 }
 
+size_t pir_ek_bytes(size_t nkeys, uint32_t logN);
+size_t eval_work_bytes(size_t nkeys, size_t ppk, uint32_t logN);
+
 int eval_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, const uint64_t* xs, size_t ppk,
                    uint32_t logN, uint8_t* out) {
     std::lock_guard<std::mutex> lk(d.mu);
@@ -181,14 +184,16 @@ int eval_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, const ui
     const uint32_t stop = stop_of(logN);
     const size_t nq = nk * ppk;
     HIP_TRY(hipError_t(d.keys.ensure(std::max<size_t>(1, nk * klen))));
-    HIP_TRY(hipError_t(d.work.ensure(std::max<size_t>(1, nk * dpfk::ek_words(stop) * 4))));
+    const size_t wbytes = eval_work_bytes(nk, ppk, logN);
+    HIP_TRY(hipError_t(d.work.ensure(std::max<size_t>(16, wbytes))));
     HIP_TRY(hipError_t(d.xs.ensure(std::max<size_t>(8, nq * 8))));
     HIP_TRY(hipError_t(d.out.ensure(std::max<size_t>(1, nq))));
     HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
     HIP_TRY(hipMemcpyAsync(d.xs.p, xs, nq * 8, hipMemcpyHostToDevice, d.st));
     HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, nk, stop, (uint32_t*)d.work.p, d.st));
+    const size_t ekb = pir_ek_bytes(nk, logN);
     HIP_TRY(dpfk::launch_eval((const uint32_t*)d.work.p, stop, logN, (const uint64_t*)d.xs.p, nq, ppk,
-                              (uint8_t*)d.out.p, d.st));
+                              (uint8_t*)d.out.p, (uint8_t*)d.work.p + ekb, wbytes - ekb, d.st));
     HIP_TRY(hipMemcpyAsync(out, d.out.p, nq, hipMemcpyDeviceToHost, d.st));
     HIP_TRY(hipStreamSynchronize(d.st));
     return DPF_OK;
@@ -223,6 +228,11 @@ int pick_ngpus(int ngpus) {
 // Expanded keys at the start of a PIR workspace, padded to 256 B.
 size_t pir_ek_bytes(size_t nkeys, uint32_t logN) {
     return (nkeys * dpfk::ek_words(stop_of(logN)) * 4 + 255) & ~(size_t)255;
+}
+
+// Batched-Eval workspace: expanded keys (256-B padded), then the frontier.
+size_t eval_work_bytes(size_t nkeys, size_t ppk, uint32_t logN) {
+    return pir_ek_bytes(nkeys, logN) + dpfk::eval_frontier_bytes(nkeys, stop_of(logN), ppk);
 }
 
 }  // namespace
@@ -351,15 +361,23 @@ int dpf_evalfull_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_
     return dpf_evalfull_subtree_dev(device, d_keys, klen, nkeys, logN, 0, 0, d_out, d_work, stream);
 }
 
+size_t dpf_eval_workspace_size(size_t nkeys, size_t pts_per_key, uint32_t logN) {
+    return std::max<size_t>(16, eval_work_bytes(nkeys, pts_per_key, logN));
+}
+
 int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, const uint64_t* d_xs,
-                       size_t ppk, uint32_t logN, uint8_t* d_out, void* d_work, void* stream) {
+                       size_t ppk, uint32_t logN, uint8_t* d_out, void* d_work, size_t work_bytes, void* stream) {
     if (int rc = check_key(klen, logN)) return rc;
     if (nkeys == 0 || ppk == 0) return DPF_OK;
     const uint32_t stop = stop_of(logN);
+    const size_t ekb = pir_ek_bytes(nkeys, logN);
+    if (work_bytes < nkeys * dpfk::ek_words(stop) * 4) return fail(DPF_ERR_PARAM, "dpf: Eval workspace too small");
     DeviceGuard g(device);
     HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop, (uint32_t*)d_work, (hipStream_t)stream));
-    HIP_TRY(dpfk::launch_eval((const uint32_t*)d_work, stop, logN, d_xs, nkeys * ppk, ppk, d_out,
-                              (hipStream_t)stream));
+    // The frontier (if it fits in the rest of the workspace) lets queries share the tree's top levels.
+    void* frontier = work_bytes > ekb ? (uint8_t*)d_work + ekb : nullptr;
+    HIP_TRY(dpfk::launch_eval((const uint32_t*)d_work, stop, logN, d_xs, nkeys * ppk, ppk, d_out, frontier,
+                              work_bytes > ekb ? work_bytes - ekb : 0, (hipStream_t)stream));
     return DPF_OK;
 }
 

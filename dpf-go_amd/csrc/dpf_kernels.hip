@@ -85,27 +85,45 @@ struct Ctx {
     uint32_t lo;
     const uint32_t* ek;
     Blk fcw;
-    uint8_t* outp;
+    uint8_t* outp;      // leaf mode: 16-byte leaf cursor
+    uint4* nseed;       // node mode: seed cursor
+    uint8_t* nt;        // node mode: t cursor
 };
+
+__device__ __forceinline__ void emit_node(Ctx& c, const Node& n) {
+    *c.nseed++ = make_uint4(n.s.c0, n.s.c1, n.s.c2, n.s.c3);
+    *c.nt++ = (uint8_t)n.t;
+}
 
 // Depth-first expansion of D more levels below node n at tree level `lvl0 +
 // (DMAX - D)`; the right child of every internal node stays live in
-// registers while the left subtree is expanded.
-template <int DMAX, int D>
+// registers while the left subtree is expanded.  Leaf mode writes the
+// converted leaves (dpf.go:214-224); node mode (NODES) writes the 2^D nodes
+// D levels down instead: the frontier a batched Eval continues from.
+template <int DMAX, int D, bool NODES>
 __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
     if constexpr (D == 0) {
-        Blk o = mmo1(c.tab, c.lo, KeyFixed<false>{}, n.s);
-        store16(c.outp, leaf_fix(o, n.t, c.fcw));
-        c.outp += 16;
+        if constexpr (NODES) {
+            emit_node(c, n);
+        } else {
+            Blk o = mmo1(c.tab, c.lo, KeyFixed<false>{}, n.s);
+            store16(c.outp, leaf_fix(o, n.t, c.fcw));
+            c.outp += 16;
+        }
     } else if constexpr (D == 1) {
         CW cw = load_cw(c.ek, lvl0 + DMAX - 1);
         Node L, R;
         expand(c.tab, c.lo, n, cw, L, R);
-        Blk oL, oR;
-        mmo2(c.tab, c.lo, KeyFixed<false>{}, L.s, oL, KeyFixed<false>{}, R.s, oR);
-        store16(c.outp, leaf_fix(oL, L.t, c.fcw));
-        store16(c.outp + 16, leaf_fix(oR, R.t, c.fcw));
-        c.outp += 32;
+        if constexpr (NODES) {
+            emit_node(c, L);
+            emit_node(c, R);
+        } else {
+            Blk oL, oR;
+            mmo2(c.tab, c.lo, KeyFixed<false>{}, L.s, oL, KeyFixed<false>{}, R.s, oR);
+            store16(c.outp, leaf_fix(oL, L.t, c.fcw));
+            store16(c.outp + 16, leaf_fix(oR, R.t, c.fcw));
+            c.outp += 32;
+        }
     } else {
         CW cw = load_cw(c.ek, lvl0 + DMAX - D);
         Node L, R;
@@ -118,7 +136,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
             ch.s.c2 = side ? R.s.c2 : L.s.c2;
             ch.s.c3 = side ? R.s.c3 : L.s.c3;
             ch.t = side ? R.t : L.t;
-            dfs<DMAX, D - 1>(c, lvl0, ch);
+            dfs<DMAX, D - 1, NODES>(c, lvl0, ch);
         }
     }
 }
@@ -153,14 +171,16 @@ __global__ void k_unpack(const uint8_t* __restrict__ keys, uint64_t key_len, uin
 // Batched / split EvalFull.  Thread u evaluates subtree `sub_base + (u mod
 // 2^units_log)` at level ltop of key (u >> units_log), a block of 2^D leaves
 // written at out + key*out_stride + (u mod 2^units_log) * 16 * 2^D.
-template <int D, bool UNIFORM>
-__global__ __launch_bounds__(kBlock, 4) void k_evalfull(const uint32_t* __restrict__ ekeys, uint32_t stop,
+// NODES: the same walk, but the 2^D nodes at level ltop + D are written to
+// (uint4*)out / out_t at [key*out_stride + (u mod 2^units_log) * 2^D].
+template <int D, bool UNIFORM, bool NODES>
+__global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                         uint64_t nunits, uint32_t units_log, uint32_t ltop,
                                                         uint64_t sub_base, uint8_t* __restrict__ out,
-                                                        uint64_t out_stride) {
+                                                        uint8_t* __restrict__ out_t, uint64_t out_stride) {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
     fill_table(s_tab);
-    const uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t u = (uint64_t)blockIdx.x * kTreeBlock + threadIdx.x;
     if (u >= nunits) return;
     uint64_t key = u >> units_log;
     if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
@@ -172,8 +192,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_evalfull(const uint32_t* __restri
     c.tab = reinterpret_cast<const uint8_t*>(s_tab);
     c.lo = (threadIdx.x & 31u) * 4u;
     c.ek = ek;
-    c.fcw = load_blk(ek + 8 + 8 * stop);
-    c.outp = out + key * out_stride + local * (16ull << D);
+    if constexpr (NODES) {
+        c.nseed = reinterpret_cast<uint4*>(out) + key * out_stride + (local << D);
+        c.nt = out_t + key * out_stride + (local << D);
+    } else {
+        c.fcw = load_blk(ek + 8 + 8 * stop);
+        c.outp = out + key * out_stride + local * (16ull << D);
+    }
 
     Node n;
     n.s = load_blk(ek);
@@ -182,15 +207,19 @@ __global__ __launch_bounds__(kBlock, 4) void k_evalfull(const uint32_t* __restri
         CW cw = load_cw(ek, i);
         walk_step(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
-    dfs<D, D>(c, ltop, n);
+    dfs<D, D, NODES>(c, ltop, n);
 }
 
-// Batched Eval: one thread per query, independent root-to-leaf walks that
-// compute only the child on the path (stop+1 AES; the reference does
-// 2*stop+1, dpf.go:183-204).  Output: one 0/1 byte per query, like Eval.
+// Batched Eval: one thread per query, independent walks that compute only
+// the child on the path (the reference computes both children, dpf.go:184).
+// Without a frontier a walk starts at the root: stop+1 AES per query.  With
+// one (fseed != nullptr) it starts from the query's level-L node, written
+// by the NODES pass: stop-L+1 AES.  Output: one 0/1 byte per query.
 __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                     uint32_t logN, const uint64_t* __restrict__ xs, uint64_t nq,
-                                                    uint64_t pts_per_key, uint8_t* __restrict__ out) {
+                                                    uint64_t pts_per_key, const uint4* __restrict__ fseed,
+                                                    const uint8_t* __restrict__ ft, uint32_t L,
+                                                    uint8_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
     fill_table(s_tab);
     const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -201,9 +230,18 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     const uint32_t lo = (threadIdx.x & 31u) * 4u;
     const uint64_t x = xs[q];
     Node n;
-    n.s = load_blk(ek);
-    n.t = ek[4];
-    for (uint32_t i = 0; i < stop; ++i) {
+    uint32_t lvl = 0;
+    if (fseed != nullptr) {
+        const uint64_t idx = (key << L) + ((x >> (logN - L)) & ((1ull << L) - 1));
+        const uint4 v = fseed[idx];
+        n.s = {v.x, v.y, v.z, v.w};
+        n.t = ft[idx];
+        lvl = L;
+    } else {
+        n.s = load_blk(ek);
+        n.t = ek[4];
+    }
+    for (uint32_t i = lvl; i < stop; ++i) {
         CW cw = load_cw(ek, i);
         walk_step(tab, lo, n, cw, (uint32_t)(x >> (logN - 1 - i)) & 1u);
     }
@@ -212,80 +250,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     const uint32_t b = (uint32_t)(x & 127);
     const uint32_t w = (b >> 5) == 0 ? o.c0 : (b >> 5) == 1 ? o.c1 : (b >> 5) == 2 ? o.c2 : o.c3;
     out[q] = (uint8_t)((w >> (b & 31)) & 1u);
-}
-
-// Batched Eval with a shared frontier: many random points of
-// one key share the top of the tree, so a workgroup first expands its key
-// breadth-first to level L (2^L nodes in LDS, 2^L - 2 AES in all instead of
-// L per query), then every query continues from its level-L node: stop - L
-// path AES + the leaf MMO.  At configs[2] (1024 points, logN=20, L=9) that
-// is 1022 + 1024*5 AES per key instead of 1024*14.  Each workgroup loops
-// over keys so the LDS table is filled once.
-template <int L>
-__global__ __launch_bounds__(kBlock, 4) void k_eval_frontier(const uint32_t* __restrict__ ekeys, uint32_t stop,
-                                                             uint32_t logN, const uint64_t* __restrict__ xs,
-                                                             uint64_t nkeys, uint64_t pts_per_key,
-                                                             uint8_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-    // Levels alternate between two node buffers, level L always in A.
-    __shared__ uint4 s_a[1 << L];
-    __shared__ uint32_t s_at[1 << L];
-    __shared__ uint4 s_b[(1 << L) / 2 > 0 ? (1 << L) / 2 : 1];
-    __shared__ uint32_t s_bt[(1 << L) / 2 > 0 ? (1 << L) / 2 : 1];
-    fill_table(s_tab);
-    const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
-    const uint32_t lo = (threadIdx.x & 31u) * 4u;
-    for (uint64_t key = blockIdx.x; key < nkeys; key += gridDim.x) {
-        const uint32_t* ek = ekeys + key * ((uint64_t)(stop + 2) * 8);
-        __syncthreads();   // previous key's queries are done with s_a
-        if (threadIdx.x == 0) {
-            Blk r = load_blk(ek);
-            ((L & 1) ? s_b : s_a)[0] = make_uint4(r.c0, r.c1, r.c2, r.c3);
-            ((L & 1) ? s_bt : s_at)[0] = ek[4];
-        }
-        // breadth-first: level d from level d-1 (d = 1..L)
-        for (int d = 1; d <= L; ++d) {
-            __syncthreads();
-            const bool to_a = ((L - d) & 1) == 0;
-            const uint4* src = to_a ? s_b : s_a;
-            const uint32_t* srct = to_a ? s_bt : s_at;
-            uint4* dst = to_a ? s_a : s_b;
-            uint32_t* dstt = to_a ? s_at : s_bt;
-            const CW cw = load_cw(ek, d - 1);
-            for (uint32_t i = threadIdx.x; i < (1u << (d - 1)); i += blockDim.x) {
-                Node n;
-                const uint4 v = src[i];
-                n.s = {v.x, v.y, v.z, v.w};
-                n.t = srct[i];
-                Node Lc, Rc;
-                expand(tab, lo, n, cw, Lc, Rc);
-                dst[2 * i] = make_uint4(Lc.s.c0, Lc.s.c1, Lc.s.c2, Lc.s.c3);
-                dst[2 * i + 1] = make_uint4(Rc.s.c0, Rc.s.c1, Rc.s.c2, Rc.s.c3);
-                dstt[2 * i] = Lc.t;
-                dstt[2 * i + 1] = Rc.t;
-            }
-        }
-        __syncthreads();
-        const Blk fcw = load_blk(ek + 8 + 8 * stop);
-        for (uint64_t q = threadIdx.x; q < pts_per_key; q += blockDim.x) {
-            const uint64_t gq = key * pts_per_key + q;
-            const uint64_t x = xs[gq];
-            const uint32_t top = (uint32_t)(x >> (logN - L)) & ((1u << L) - 1);
-            Node n;
-            const uint4 v = s_a[top];
-            n.s = {v.x, v.y, v.z, v.w};
-            n.t = s_at[top];
-            for (uint32_t i = L; i < stop; ++i) {
-                CW cw = load_cw(ek, i);
-                walk_step(tab, lo, n, cw, (uint32_t)(x >> (logN - 1 - i)) & 1u);
-            }
-            Blk o = mmo1(tab, lo, KeyFixed<false>{}, n.s);
-            o = leaf_fix(o, n.t, fcw);
-            const uint32_t b = (uint32_t)(x & 127);
-            const uint32_t w = (b >> 5) == 0 ? o.c0 : (b >> 5) == 1 ? o.c1 : (b >> 5) == 2 ? o.c2 : o.c3;
-            out[gq] = (uint8_t)((w >> (b & 31)) & 1u);
-        }
-    }
 }
 
 // ------------------------------------------------------------ launchers ---
@@ -299,18 +263,26 @@ hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, 
     return hipGetLastError();
 }
 
-template <int D>
+template <int D, bool NODES>
 static hipError_t launch_full_d(const uint32_t* ek, uint32_t stop, uint64_t nunits, uint32_t units_log,
-                                uint32_t ltop, uint64_t sub_base, uint8_t* out, uint64_t out_stride,
-                                hipStream_t st) {
-    const uint64_t blocks = (nunits + kBlock - 1) / kBlock;
+                                uint32_t ltop, uint64_t sub_base, uint8_t* out, uint8_t* out_t,
+                                uint64_t out_stride, hipStream_t st) {
+    const uint64_t blocks = (nunits + kTreeBlock - 1) / kTreeBlock;
     if (units_log >= 6)
-        hipLaunchKernelGGL((k_evalfull<D, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, st, ek, stop, nunits,
-                           units_log, ltop, sub_base, out, out_stride);
+        hipLaunchKernelGGL((k_evalfull<D, true, NODES>), dim3((uint32_t)blocks), dim3(kTreeBlock), 0, st, ek, stop,
+                           nunits, units_log, ltop, sub_base, out, out_t, out_stride);
     else
-        hipLaunchKernelGGL((k_evalfull<D, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, st, ek, stop, nunits,
-                           units_log, ltop, sub_base, out, out_stride);
+        hipLaunchKernelGGL((k_evalfull<D, false, NODES>), dim3((uint32_t)blocks), dim3(kTreeBlock), 0, st, ek, stop,
+                           nunits, units_log, ltop, sub_base, out, out_t, out_stride);
     return hipGetLastError();
+}
+
+static int cu_count() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return cus;
 }
 
 // Per-thread subtree depth.  Deeper subtrees amortise the root-to-subtree
@@ -325,69 +297,83 @@ static uint32_t pick_depth(uint32_t span, uint64_t nkeys) {
     }();
     uint32_t d = span < kMaxD ? span : kMaxD;
     if (forced >= 0) return span < (uint32_t)forced ? span : (uint32_t)forced;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const uint64_t fill = (uint64_t)cus * 2 * kBlock;
+    const uint64_t fill = (uint64_t)cu_count() * 2 * kTreeBlock;
     auto threads = [&](uint32_t dd) { return span - dd >= 40 ? ~0ull : nkeys << (span - dd); };
     while (d > kMinD && threads(d) < fill) --d;
     return d;
 }
 
-hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
-                           uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st) {
-    const uint32_t span = stop - prefix_bits;          // levels below the prefix node
-    const uint32_t d = pick_depth(span, nkeys);         // per-thread subtree depth
-    const uint32_t ltop = stop - d;                     // levels walked per thread
-    const uint32_t units_log = ltop - prefix_bits;      // threads per key = 2^units_log
+// Tree pass over every key: leaves of the subtree (prefix_bits, prefix) when
+// NODES is false, the 2^depth nodes at level `depth` (prefix 0) when true.
+template <bool NODES>
+static hipError_t launch_tree(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t depth,
+                              uint32_t prefix_bits, uint64_t prefix, uint8_t* out, uint8_t* out_t,
+                              uint64_t out_stride, hipStream_t st) {
+    const uint32_t span = depth - prefix_bits;          // levels below the prefix node
+    const uint32_t d = pick_depth(span, nkeys);          // per-thread subtree depth
+    const uint32_t ltop = depth - d;                     // levels walked per thread
+    const uint32_t units_log = ltop - prefix_bits;       // threads per key = 2^units_log
     const uint64_t nunits = nkeys << units_log;
     const uint64_t sub_base = prefix << units_log;
     if (nunits == 0) return hipSuccess;
+#define DPF_LAUNCH(DD) \
+    return launch_full_d<DD, NODES>(ek, stop, nunits, units_log, ltop, sub_base, out, out_t, out_stride, st)
     switch (d) {
-        case 0: return launch_full_d<0>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
-        case 1: return launch_full_d<1>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
-        case 2: return launch_full_d<2>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
-        case 3: return launch_full_d<3>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
-        case 4: return launch_full_d<4>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
-        case 5: return launch_full_d<5>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
-        case 6: return launch_full_d<6>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
-        default: return launch_full_d<7>(ek, stop, nunits, units_log, ltop, sub_base, out, out_stride, st);
+        case 0: DPF_LAUNCH(0);
+        case 1: DPF_LAUNCH(1);
+        case 2: DPF_LAUNCH(2);
+        case 3: DPF_LAUNCH(3);
+        case 4: DPF_LAUNCH(4);
+        case 5: DPF_LAUNCH(5);
+        case 6: DPF_LAUNCH(6);
+        default: DPF_LAUNCH(7);
     }
+#undef DPF_LAUNCH
 }
 
-template <int L>
-static hipError_t launch_frontier(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs,
-                                  uint64_t nkeys, uint64_t ppk, uint8_t* out, hipStream_t st) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const uint64_t grid = nkeys < (uint64_t)cus * 2 ? nkeys : (uint64_t)cus * 2;
-    hipLaunchKernelGGL((k_eval_frontier<L>), dim3((uint32_t)grid), dim3(kBlock), 0, st, ek, stop, logN, xs, nkeys,
-                       ppk, out);
-    return hipGetLastError();
+hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
+                           uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st) {
+    return launch_tree<false>(ek, nkeys, stop, stop, prefix_bits, prefix, out, nullptr, out_stride, st);
+}
+
+uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key) {
+    // Shared frontier at level L when a key's points cover it: 2^(L+1) <= ppk.
+    uint32_t L = 0;
+    while (L < kMaxFrontierHbm && L < stop && (2ull << (L + 1)) <= pts_per_key) ++L;
+    return L >= 4 ? L : 0;
+}
+
+uint64_t eval_frontier_bytes(uint64_t nkeys, uint32_t stop, uint64_t pts_per_key) {
+    const uint32_t L = eval_frontier_level(stop, pts_per_key);
+    if (L == 0) return 0;
+    return ((nkeys << L) * 16 + (nkeys << L) + 255) & ~255ull;
 }
 
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
-                       uint64_t pts_per_key, uint8_t* out, hipStream_t st) {
+                       uint64_t pts_per_key, uint8_t* out, void* frontier, uint64_t frontier_bytes,
+                       hipStream_t st) {
     if (nq == 0) return hipSuccess;
-    // Shared frontier at level L when a key's points cover it: 2^L <= ppk / 2.
-    static const bool no_frontier = getenv("DPF_EVAL_NO_FRONTIER") != nullptr;
-    uint32_t L = 0;
-    while (L < kMaxFrontier && L < stop && (2ull << (L + 1)) <= pts_per_key) ++L;
-    if (!no_frontier && L >= 6) {
-        const uint64_t nkeys = nq / pts_per_key;
-        switch (L) {
-            case 6: return launch_frontier<6>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
-            case 7: return launch_frontier<7>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
-            case 8: return launch_frontier<8>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
-            default: return launch_frontier<9>(ek, stop, logN, xs, nkeys, pts_per_key, out, st);
-        }
+    // DPF_EVAL_MODE=plain forces root walks (measurement only).
+    static const bool plain = [] {
+        const char* e = getenv("DPF_EVAL_MODE");
+        return e && e[0] == 'p';
+    }();
+    const uint64_t nkeys = nq / pts_per_key;
+    uint32_t L = eval_frontier_level(stop, pts_per_key);
+    if (plain || frontier == nullptr || frontier_bytes < eval_frontier_bytes(nkeys, stop, pts_per_key)) L = 0;
+    const uint4* fseed = nullptr;
+    const uint8_t* ft = nullptr;
+    if (L > 0) {
+        uint8_t* fs = static_cast<uint8_t*>(frontier);
+        uint8_t* fts = fs + (nkeys << L) * 16;
+        hipError_t e = launch_tree<true>(ek, nkeys, stop, L, 0, 0, fs, fts, 1ull << L, st);
+        if (e != hipSuccess) return e;
+        fseed = reinterpret_cast<const uint4*>(fs);
+        ft = fts;
     }
     const uint64_t blocks = (nq + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_eval, dim3((uint32_t)blocks), dim3(kBlock), 0, st, ek, stop, logN, xs, nq, pts_per_key,
-                       out);
+                       fseed, ft, L, out);
     return hipGetLastError();
 }
 

@@ -6,9 +6,19 @@
 namespace dpfk {
 
 constexpr int kBlock = 512;    // threads per workgroup (8 waves); 2 workgroups per CU (64 KiB LDS table each)
+#ifndef DPF_TREE_BLOCK
+#define DPF_TREE_BLOCK 512
+#endif
+#ifndef DPF_TREE_WAVES
+#define DPF_TREE_WAVES 4
+#endif
+// Tree kernel geometry: 2 workgroups of kTreeBlock threads per CU (LDS-bound),
+// kTreeWaves waves per SIMD (VGPR budget).  Build-time knobs for A/B runs.
+constexpr int kTreeBlock = DPF_TREE_BLOCK;
+constexpr int kTreeWaves = DPF_TREE_WAVES;
 constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
 constexpr uint32_t kMinD = 5;  // smallest depth chosen to fill the GPU (walk overhead <= ~13%)
-constexpr uint32_t kMaxFrontier = 9;  // batched Eval: deepest shared level kept in LDS (512 nodes)
+constexpr uint32_t kMaxFrontierHbm = 16;  // batched Eval, HBM frontier: deepest shared level
 
 // Expanded-key words per key: (stop + 2) records of 8 u32.
 inline uint64_t ek_words(uint32_t stop) { return ((uint64_t)stop + 2) * 8; }
@@ -22,7 +32,14 @@ hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, 
 hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
                            uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st);
 
+// Batched Eval.  When a key has enough points to share the top of its tree
+// (2^(L+1) <= pts_per_key), the 2^L nodes at level L of every key are first
+// computed into `frontier` (eval_frontier_bytes of it) and each query starts
+// there; with frontier == nullptr (or too small) every walk starts at the root.
+uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key);
+uint64_t eval_frontier_bytes(uint64_t nkeys, uint32_t stop, uint64_t pts_per_key);
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
-                       uint64_t pts_per_key, uint8_t* out, hipStream_t st);
+                       uint64_t pts_per_key, uint8_t* out, void* frontier, uint64_t frontier_bytes,
+                       hipStream_t st);
 
 }  // namespace dpfk

@@ -23,7 +23,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdpf_hip.so")
+LIB_PATH = os.environ.get("DPF_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libdpf_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "dpf_hip.h")
 
 DPF_OK = 0
@@ -69,7 +69,8 @@ SIGNATURES = {
     "dpf_evalfull_split": (_int, [_u8p, _sz, _u32, _u8p, _int]),
     "dpf_evalfull_batch_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp, _vp]),
     "dpf_evalfull_subtree_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _vp, _vp]),
-    "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _vp]),
+    "dpf_eval_workspace_size": (_sz, [_sz, _sz, _u32]),
+    "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _sz, _vp]),
     "dpf_expand_keys_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp]),
     "dpf_evalfull_expanded_dev": (_int, [_int, _vp, _sz, _u32, _u32, _u64, _vp, _vp]),
     "dpf_pir_workspace_size": (_sz, [_sz, _u32, _u32]),
@@ -248,10 +249,16 @@ def evalfull_subtree_dev(d_keys, key_len_: int, nkeys: int, logN: int, prefix_bi
                                           _ptr(d_out), _ptr(d_work), _stream_handle(stream)))
 
 
+def eval_workspace_size(nkeys: int, pts_per_key: int, logN: int) -> int:
+    return int(lib().dpf_eval_workspace_size(nkeys, pts_per_key, logN))
+
+
 def eval_batch_dev(d_keys, key_len_: int, nkeys: int, d_xs, pts_per_key: int, logN: int, d_out, d_work,
                    device: int = 0, stream=None) -> None:
+    """Batched Eval on HBM tensors; d_work's size picks root walks or a shared frontier."""
+    nbytes = int(d_work.numel() * d_work.element_size())
     _check(lib().dpf_eval_batch_dev(device, _ptr(d_keys), key_len_, nkeys, _ptr(d_xs), pts_per_key, logN,
-                                    _ptr(d_out), _ptr(d_work), _stream_handle(stream)))
+                                    _ptr(d_out), _ptr(d_work), nbytes, _stream_handle(stream)))
 
 
 def expand_keys_dev(d_keys, key_len_: int, nkeys: int, logN: int, d_work, device: int = 0, stream=None) -> None:

@@ -94,8 +94,15 @@ int dpf_evalfull_batch_dev(int device, const uint8_t* d_keys, size_t key_len, si
  * prefix_bits) bytes per key at d_out + k*that (logN-7 >= prefix_bits). */
 int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, uint32_t logN,
                              uint32_t prefix_bits, uint64_t prefix, uint8_t* d_out, void* d_work, void* stream);
+/* Batched Eval on HBM buffers.  d_work holds work_bytes; with
+ * dpf_eval_workspace_size(nkeys, pts_per_key, logN) bytes the queries of a
+ * key share its top tree levels (a frontier of 2^L nodes per key computed
+ * once); with only dpf_workspace_size(nkeys, logN) bytes each query walks
+ * from the root.  Results are identical either way. */
+size_t dpf_eval_workspace_size(size_t nkeys, size_t pts_per_key, uint32_t logN);
 int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, const uint64_t* d_xs,
-                       size_t pts_per_key, uint32_t logN, uint8_t* d_out, void* d_work, void* stream);
+                       size_t pts_per_key, uint32_t logN, uint8_t* d_out, void* d_work, size_t work_bytes,
+                       void* stream);
 
 /* Two-phase form of the above: expand keys once into d_work (the aligned
  * per-level records the kernels read), then evaluate any number of
