@@ -128,10 +128,16 @@ class Ctx:
         self.args = args
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # One rank per GPU.  DPF_BENCH_BACKEND=gloo plus ranks folded onto the
+        # visible devices lets the multi-rank path run on a 1-GPU box (test only).
+        self.backend = os.environ.get("DPF_BENCH_BACKEND", "nccl")
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         if self.world > 1:
             torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group(self.backend)
         self.dev = torch.device("cuda", self.local)
         torch.cuda.set_device(self.dev)
         dpf.gpu_init(0)
@@ -156,7 +162,8 @@ class Ctx:
             dist.barrier()
         t_wall = time.perf_counter() - t0
         if self.world > 1:
-            t = torch.tensor([t_wall], dtype=torch.float64, device=self.dev)
+            t = torch.tensor([t_wall], dtype=torch.float64,
+                             device=self.dev if self.backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             t_wall = float(t.item())
         k_ms = sum(a.elapsed_time(b) for a, b in evs) / steps

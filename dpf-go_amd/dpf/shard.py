@@ -49,6 +49,8 @@ def gather_xor(partial, group=None) -> np.ndarray:
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo" and partial.is_cuda:
+        partial = partial.cpu()
     bufs = [torch.empty_like(partial) for _ in range(world)]
     dist.all_gather(bufs, partial, group=group)
     return xor_fold(np.stack([b.cpu().numpy() for b in bufs]))
