@@ -25,15 +25,59 @@
 namespace dpfk {
 
 constexpr int kFoldWaves = 4;
-constexpr int kFoldR = 8;        // records per lane held in registers
+#ifndef DPF_FOLD_R
+#define DPF_FOLD_R 8
+#endif
+#ifndef DPF_FOLD_SHFL
+#define DPF_FOLD_SHFL 0
+#endif
+constexpr int kFoldR = DPF_FOLD_R;   // records per lane held in registers (build knob: 8 or 16)
 constexpr int kFoldMaxB = 64;    // keys per launch (LDS combine buffer)
 
 __device__ __forceinline__ uint32_t xorsel(uint32_t acc, uint32_t rec, uint32_t m) {
     return __builtin_amdgcn_bitop3_b32(acc, rec, m, 0x78);   // acc ^ (rec & m): 0xF0 ^ (0xCC & 0xAA)
 }
 
+// DPP lane moves (VALU, no LDS): row_ror:8 = lane ^ 8 within a 16-lane row,
+// row_half_mirror = lane -> 7 - lane within 8, quad_perm [1,0,3,2] / [2,3,0,1].
+__device__ __forceinline__ uint32_t dpp_ror8(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_half_mirror(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_quad(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+
 // XOR-reduce v[0..7] over the 64 lanes; afterwards lane l holds the full
-// reduction of word (l >> 3) & 7 in v[0].
+// reduction of word (l >> 3) & 7 in v[0].  Register-halving butterfly on
+// VALU-only lane exchanges: v_permlane32_swap (lanes l <-> l^32), then
+// v_permlane16_swap (l <-> l^16 within each half), DPP row_ror:8 (l^8),
+// and a 3-step DPP reduction inside each group of 8 lanes.
+__device__ __forceinline__ uint32_t wave_xor8_dpp(uint32_t v[8]) {
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {       // word i + 4*(l>>5)
+        auto r = __builtin_amdgcn_permlane32_swap(v[i], v[4 + i], false, false);
+        v[i] = r[0] ^ r[1];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {       // word i + 2*((l>>4)&1) + 4*(l>>5)
+        auto r = __builtin_amdgcn_permlane16_swap(v[i], v[2 + i], false, false);
+        v[i] = r[0] ^ r[1];
+    }
+    const bool hi = l & 8;              // word (l>>3)&7
+    const uint32_t keep = hi ? v[1] : v[0], send = hi ? v[0] : v[1];
+    uint32_t x = keep ^ dpp_ror8(send);
+    x ^= dpp_half_mirror(x);            // pairs (j, 7-j) within 8 lanes
+    x ^= dpp_quad<0xB1>(x);             // quad_perm [1,0,3,2]
+    x ^= dpp_quad<0x4E>(x);             // quad_perm [2,3,0,1]
+    return x;
+}
+
+// Reference form of the same reduction over __shfl_xor (kept for A/B).
 __device__ __forceinline__ uint32_t wave_xor8(uint32_t v[8]) {
     const int l = threadIdx.x & 63;
     // step 1: lanes l and l^32 trade halves, each keeps 4 words
@@ -113,7 +157,11 @@ __global__ __launch_bounds__(64 * kFoldWaves) void k_pir_fold(const uint32_t* __
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[i] = xorsel(acc[i], rec[j][i], m);
         }
+#if DPF_FOLD_SHFL
         const uint32_t red = wave_xor8(acc);
+#else
+        const uint32_t red = wave_xor8_dpp(acc);
+#endif
         if ((l & 7) == 0) s_part[w][k][l >> 3] = red;
     }
     __syncthreads();
