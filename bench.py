@@ -84,9 +84,17 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float) ->
         "hbm_GBs": round(gbs, 1),
         "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
     }
-    tr = os.environ.get("DPF_TRAFFIC_BYTES")
-    if tr:
-        r["traffic"] = float(tr)
+    # Measured HBM bytes per launch of this kernel from the committed PMC
+    # passes (tools/counters.sh + tools/traffic.py -> profiles/r01_traffic.json).
+    try:
+        with open(os.path.join(ROOT, "profiles", "r01_traffic.json")) as f:
+            t = json.load(f)
+        key = kernel
+        if key in t:
+            r["traffic"] = round(t[key]["traffic_bytes"])
+            r["traffic_over_algorithmic"] = round(t[key]["traffic_bytes"] / hbm_bytes, 3)
+    except Exception:
+        pass
     return r
 
 
@@ -211,7 +219,7 @@ def wl_evalfull(c: Ctx) -> dict:
                           "keys_per_gpu": nk, "logN": logN, "aes": "lds-ttable",
                           "parallelism": f"key-shard x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), f"k_evalfull<{min(stop_of(logN), 7)},true>", k_ms,
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), f"k_evalfull<{min(stop_of(logN), 7)}, true, false>", k_ms,
                                     nk * olen + nk * (stop_of(logN) + 2) * 32)
     return line
 
