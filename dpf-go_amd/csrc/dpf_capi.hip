@@ -288,6 +288,7 @@ int dpf_gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s
 
 int dpf_evalfull_batch(const uint8_t* keys, size_t klen, size_t nkeys, uint32_t logN, uint8_t* out, int ngpus) {
     if (int rc = check_key(klen, logN)) return rc;
+    if (nkeys == 0) return DPF_OK;
     const int g = pick_ngpus(ngpus);
     if (g <= 0) return g;
     const size_t olen = full_len(logN);
@@ -303,6 +304,7 @@ int dpf_evalfull(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out) {
 int dpf_eval_batch(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_t* xs, size_t ppk, uint32_t logN,
                    uint8_t* out, int ngpus) {
     if (int rc = check_key(klen, logN)) return rc;
+    if (nkeys == 0 || ppk == 0) return DPF_OK;
     const int g = pick_ngpus(ngpus);
     if (g <= 0) return g;
     return shard(nkeys, g, [&](int dev, size_t lo, size_t hi) {

@@ -86,3 +86,35 @@ def test_synth_is_deterministic():
     assert int(a[0].max()) < (1 << 20)
     assert synth.eval_points(4, 16, 20).max() < (1 << 20)
     assert synth.db_bytes(100).shape == (100,)
+
+
+def _build_c_smoke(tmp_path):
+    """Compile tests/c/capi_smoke.c against include/dpf_hip.h with plain gcc
+    (C99, -Werror): the header is C-clean and every symbol the program uses
+    resolves from the shared library at link time."""
+    import shutil
+    import subprocess
+    gcc = shutil.which("gcc") or shutil.which("cc")
+    if gcc is None:
+        pytest.skip("no C compiler")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libdir = os.path.dirname(dpf.LIB_PATH)
+    exe = str(tmp_path / "capi_smoke")
+    subprocess.run([gcc, "-std=c99", "-O1", "-Wall", "-Werror", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "c", "capi_smoke.c"), "-o", exe, "-L", libdir, "-ldpf_hip",
+                    "-Wl,-rpath," + libdir], check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_c_program_links_against_header(tmp_path):
+    assert os.path.exists(_build_c_smoke(tmp_path))
+
+
+@pytest.mark.gpu
+def test_c_program_runs_on_gpu(tmp_path):
+    """The same checks as the reference's dpf_test.go, from C through the ABI."""
+    import subprocess
+    exe = _build_c_smoke(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all checks passed" in r.stdout

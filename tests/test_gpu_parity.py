@@ -227,3 +227,49 @@ def test_eval_frontier_path_vs_oracle(logN, nk, ppk):
     got = dpf.eval_batch(ka, xs, logN, ngpus=1)
     want = oracle.eval_batch(ka, xs, logN, nthreads=NT)
     assert np.array_equal(got, want)
+
+
+def test_empty_and_degenerate_inputs():
+    """Empty batches are no-ops; invalid splits and undersized workspaces
+    fail with an error code instead of touching memory."""
+    import torch
+    logN = 12
+    kl = dpf.key_len(logN)
+    none = np.zeros((0, kl), np.uint8)
+    assert dpf.evalfull_batch(none, logN, ngpus=1).shape == (0, dpf.evalfull_len(logN))
+    assert dpf.eval_batch(none, np.zeros((0, 5), np.uint64), logN, ngpus=1).shape == (0, 5)
+    _, ka, kb = _keys(3, logN, first=31337)
+    assert dpf.eval_batch(ka, np.zeros((3, 0), np.uint64), logN, ngpus=1).shape == (3, 0)
+    _, k20, _ = _keys(1, 20, first=31338)
+    with pytest.raises(dpf.DPFPanic) as e:
+        dpf.evalfull_split(k20[0].tobytes(), 20, 3)
+    assert e.value.code == dpf.DPF_ERR_PARAM
+    dev = torch.device("cuda", 0)
+    d_keys = torch.from_numpy(ka.reshape(-1)).to(dev)
+    d_xs = torch.zeros(3 * 4, dtype=torch.int64, device=dev)
+    d_out = torch.zeros(3 * 4, dtype=torch.uint8, device=dev)
+    tiny = torch.empty(8, dtype=torch.uint8, device=dev)
+    with pytest.raises(dpf.DPFPanic) as e:
+        dpf.eval_batch_dev(d_keys, kl, 3, d_xs, 4, logN, d_out, tiny, stream=torch.cuda.current_stream(dev))
+    assert e.value.code == dpf.DPF_ERR_PARAM
+    # a workspace of exactly the key-expansion size takes the plain path
+    from dpf import eval_workspace_size
+    need = eval_workspace_size(3, 4, logN)
+    d_work = torch.empty(need, dtype=torch.uint8, device=dev)
+    dpf.eval_batch_dev(d_keys, kl, 3, d_xs, 4, logN, d_out, d_work, stream=torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    want = oracle.eval_batch(ka, np.zeros((3, 4), np.uint64), logN, nthreads=1)
+    assert np.array_equal(d_out.cpu().numpy().reshape(3, 4), want)
+
+
+@pytest.mark.parametrize("logN", [0, 1, 6, 7, 8])
+def test_tiny_domains_all_points(logN):
+    """Domains below and at the 2^7 leaf block (stop = 0 / 1): every point of
+    Eval and EvalFull against the oracle, both shares."""
+    al, ka, kb = _keys(9, logN, first=logN * 100)
+    xs = np.tile(np.arange(1 << logN, dtype=np.uint64), (9, 1))
+    for k in (ka, kb):
+        assert np.array_equal(dpf.eval_batch(k, xs, logN, ngpus=1), oracle.eval_batch(k, xs, logN, nthreads=1))
+        assert np.array_equal(dpf.evalfull_batch(k, logN, ngpus=1), oracle.evalfull_batch(k, logN, nthreads=1))
+    got = dpf.eval_batch(ka, xs, logN, ngpus=1) ^ dpf.eval_batch(kb, xs, logN, ngpus=1)
+    assert np.array_equal(got, (xs == al[:, None]).astype(np.uint8))
