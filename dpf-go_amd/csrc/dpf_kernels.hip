@@ -12,6 +12,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+
+#include <algorithm>
+#include <cmath>
 #include "aes_consts.hpp"
 #include "aes_ttable.hpp"
 #include "dpf_kernels.hpp"
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
                                                         uint8_t* __restrict__ out_t, uint64_t out_stride) {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
     fill_table(s_tab);
-    const uint64_t u = (uint64_t)blockIdx.x * kTreeBlock + threadIdx.x;
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kTreeBlock
     if (u >= nunits) return;
     uint64_t key = u >> units_log;
     if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
                                                     uint8_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
     fill_table(s_tab);
-    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kBlock
     if (q >= nq) return;
     const uint64_t key = q / pts_per_key;
     const uint32_t* ek = ekeys + key * ((uint64_t)(stop + 2) * 8);
@@ -288,13 +291,13 @@ hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, 
 template <int D, bool NODES>
 static hipError_t launch_full_d(const uint32_t* ek, uint32_t stop, uint64_t nunits, uint32_t units_log,
                                 uint32_t ltop, uint64_t sub_base, uint8_t* out, uint8_t* out_t,
-                                uint64_t out_stride, hipStream_t st) {
-    const uint64_t blocks = (nunits + kTreeBlock - 1) / kTreeBlock;
+                                uint64_t out_stride, uint32_t block, hipStream_t st) {
+    const uint64_t blocks = (nunits + block - 1) / block;
     if (units_log >= 6)
-        hipLaunchKernelGGL((k_evalfull<D, true, NODES>), dim3((uint32_t)blocks), dim3(kTreeBlock), 0, st, ek, stop,
+        hipLaunchKernelGGL((k_evalfull<D, true, NODES>), dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop,
                            nunits, units_log, ltop, sub_base, out, out_t, out_stride);
     else
-        hipLaunchKernelGGL((k_evalfull<D, false, NODES>), dim3((uint32_t)blocks), dim3(kTreeBlock), 0, st, ek, stop,
+        hipLaunchKernelGGL((k_evalfull<D, false, NODES>), dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop,
                            nunits, units_log, ltop, sub_base, out, out_t, out_stride);
     return hipGetLastError();
 }
@@ -307,22 +310,58 @@ static int cu_count() {
     return cus;
 }
 
-// Per-thread subtree depth.  Deeper subtrees amortise the root-to-subtree
-// walk (ltop AES per thread against 3*2^D - 2), but a small batch of keys
-// then launches too few threads to fill the GPU; shrink D (not below kMinD)
-// until the grid reaches two 512-thread workgroups per CU.
+// Workgroup size for a grid of n threads: full kTreeBlock-thread groups once
+// the grid covers every CU, otherwise the smallest power of two (>= one
+// wave) that spreads it over all CUs, so that a small batch is not packed
+// onto a few CUs whose LDS pipe then serialises it.
+static uint32_t pick_block(uint64_t n, uint32_t maxb) {
+    const uint64_t cus = (uint64_t)cu_count();
+    uint32_t b = 64;
+    while (b < maxb && n > cus * b) b <<= 1;
+    return b;
+}
+
+// Per-thread subtree depth D and workgroup size.  A thread walks span - D
+// levels (one AES each) and expands 3 * 2^D - 2 AES depth-first: deeper
+// subtrees amortise the walk, shallower ones give more, shorter threads.
+// Time model fitted to tools/exp_latency.sh on MI355X (all batch shapes
+// within ~8%): a thread's AES take max(kLat, w * kPerWave) each, w = waves
+// per CU (<= 16; more threads run in further rounds).  The throughput regime
+// (4096 keys x logN=20) takes D = 7; one key at logN=20 takes D = 0, 14 AES
+// deep per thread instead of 197 at D = 7.
 // DPF_SUBTREE_DEPTH overrides the choice (measurement only).
-static uint32_t pick_depth(uint32_t span, uint64_t nkeys) {
+struct TreeShape {
+    uint32_t d, block;
+};
+static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes) {
     static const int forced = [] {
         const char* e = getenv("DPF_SUBTREE_DEPTH");
         return e ? atoi(e) : -1;
     }();
-    uint32_t d = span < kMaxD ? span : kMaxD;
-    if (forced >= 0) return span < (uint32_t)forced ? span : (uint32_t)forced;
-    const uint64_t fill = (uint64_t)cu_count() * 2 * kTreeBlock;
+    const uint32_t dmax = span < kMaxD ? span : kMaxD;
     auto threads = [&](uint32_t dd) { return span - dd >= 40 ? ~0ull : nkeys << (span - dd); };
-    while (d > kMinD && threads(d) < fill) --d;
-    return d;
+    if (forced >= 0) {
+        const uint32_t d = dmax < (uint32_t)forced ? dmax : (uint32_t)forced;
+        return {d, pick_block(threads(d), kTreeBlock)};
+    }
+    constexpr double kLat = 1.9e-6;       // one AES-MMO of a thread on a lightly loaded CU
+    constexpr double kPerWave = 0.2e-6;   // ... per resident wave when the CU's LDS pipe is shared
+    const double wave_slots = 64.0 * cu_count();
+    uint32_t best = dmax;
+    double best_t = 1e30;
+    for (int dd = (int)dmax; dd >= 0; --dd) {
+        const uint32_t d = (uint32_t)dd;
+        const double work = (double)(span - d) + (nodes ? 2.0 : 3.0) * (double)(1u << d) - 2.0;   // NODES: no leaf AES
+        const double w = (double)threads(d) / wave_slots;                 // waves per CU
+        const double rounds = w > 16.0 ? std::ceil(w / 16.0) : 1.0;
+        const double per = w > 16.0 ? 16.0 * kPerWave : std::max(kLat, w * kPerWave);
+        const double t = rounds * work * std::max(kLat, per);
+        if (t < best_t * 0.98) {          // prefer the deeper subtree on near-ties (less total work)
+            best_t = t;
+            best = d;
+        }
+    }
+    return {best, pick_block(threads(best), kTreeBlock)};
 }
 
 // Tree pass over every key: leaves of the subtree (prefix_bits, prefix) when
@@ -332,14 +371,15 @@ static hipError_t launch_tree(const uint32_t* ek, uint64_t nkeys, uint32_t stop,
                               uint32_t prefix_bits, uint64_t prefix, uint8_t* out, uint8_t* out_t,
                               uint64_t out_stride, hipStream_t st) {
     const uint32_t span = depth - prefix_bits;          // levels below the prefix node
-    const uint32_t d = pick_depth(span, nkeys);          // per-thread subtree depth
+    const TreeShape sh = pick_shape(span, nkeys, NODES);
+    const uint32_t d = sh.d;                             // per-thread subtree depth
     const uint32_t ltop = depth - d;                     // levels walked per thread
     const uint32_t units_log = ltop - prefix_bits;       // threads per key = 2^units_log
     const uint64_t nunits = nkeys << units_log;
     const uint64_t sub_base = prefix << units_log;
     if (nunits == 0) return hipSuccess;
 #define DPF_LAUNCH(DD) \
-    return launch_full_d<DD, NODES>(ek, stop, nunits, units_log, ltop, sub_base, out, out_t, out_stride, st)
+    return launch_full_d<DD, NODES>(ek, stop, nunits, units_log, ltop, sub_base, out, out_t, out_stride, sh.block, st)
     switch (d) {
         case 0: DPF_LAUNCH(0);
         case 1: DPF_LAUNCH(1);
@@ -393,8 +433,9 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
         fseed = reinterpret_cast<const uint4*>(fs);
         ft = fts;
     }
-    const uint64_t blocks = (nq + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_eval, dim3((uint32_t)blocks), dim3(kBlock), 0, st, ek, stop, logN, xs, nq, pts_per_key,
+    const uint32_t block = pick_block(nq, kBlock);
+    const uint64_t blocks = (nq + block - 1) / block;
+    hipLaunchKernelGGL(k_eval, dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop, logN, xs, nq, pts_per_key,
                        fseed, ft, L, out);
     return hipGetLastError();
 }

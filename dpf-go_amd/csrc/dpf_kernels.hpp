@@ -17,7 +17,6 @@ constexpr int kBlock = 512;    // threads per workgroup (8 waves); 2 workgroups 
 constexpr int kTreeBlock = DPF_TREE_BLOCK;
 constexpr int kTreeWaves = DPF_TREE_WAVES;
 constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
-constexpr uint32_t kMinD = 5;  // smallest depth chosen to fill the GPU (walk overhead <= ~13%)
 constexpr uint32_t kMaxFrontierHbm = 16;  // batched Eval, HBM frontier: deepest shared level
 
 // Expanded-key words per key: (stop + 2) records of 8 u32.

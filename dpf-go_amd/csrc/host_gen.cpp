@@ -4,6 +4,7 @@
 // T-table software AES when the CPU lacks AES-NI.  Batched generation over
 // host threads is SURVEY §8(f)1.
 #include <errno.h>
+#include <sched.h>
 #include <stdint.h>
 #include <string.h>
 #include <sys/random.h>
@@ -153,14 +154,22 @@ int gen_random(uint64_t alpha, uint32_t logN, uint8_t* ka, uint8_t* kb) {
     return gen_seeded(alpha, logN, seeds, seeds + 16, ka, kb);
 }
 
+static int usable_cpus() {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) return std::max(1, CPU_COUNT(&set));
+    return (int)std::max(1u, std::thread::hardware_concurrency());
+}
+
 int gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, const uint8_t* s1s, size_t n,
                      uint8_t* kas, uint8_t* kbs, int nthreads) {
     if (logN > 63) return DPF_ERR_PARAM;
     for (size_t i = 0; i < n; ++i)
         if (alphas[i] >= (1ull << logN)) return DPF_ERR_PARAM;
     const size_t kl = 33 + 18 * (size_t)(logN >= 7 ? logN - 7 : 0);
-    int nt = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
-    nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(n, 1));
+    // Default: the CPUs this process may run on, at most 32; and no more
+    // threads than 512-key chunks (a key pair takes ~1-3 us, a thread ~30 us).
+    int nt = nthreads > 0 ? nthreads : std::min(32, usable_cpus());
+    nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>((n + 511) / 512, 1));
     auto work = [&](int tid) {
         for (size_t i = (size_t)tid; i < n; i += (size_t)nt)
             gen_seeded(alphas[i], logN, s0s + 16 * i, s1s + 16 * i, kas + kl * i, kbs + kl * i);
