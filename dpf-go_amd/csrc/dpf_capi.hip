@@ -409,7 +409,7 @@ int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint
 size_t dpf_pir_workspace_size(size_t nkeys, uint32_t logN, uint32_t prefix_bits) {
     const uint32_t stop = stop_of(logN);
     const uint32_t pb = prefix_bits > stop ? stop : prefix_bits;
-    return pir_ek_bytes(nkeys, logN) + nkeys * ((size_t)16 << (stop - pb));
+    return pir_ek_bytes(nkeys, logN) + nkeys * ((size_t)16 << (stop - pb)) + dpfk::pir_fold_parts_bytes();
 }
 
 int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN,
@@ -429,7 +429,8 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
     int rc = enqueue_full(d_keys, klen, nkeys, logN, prefix_bits, prefix, bits, ek, st);
     if (rc) return rc;
-    HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, (uint32_t)nkeys, (uint32_t*)d_ans,
+    uint32_t* parts = (uint32_t*)(bits + nkeys * per_key);
+    HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, (uint32_t)nkeys, (uint32_t*)d_ans, parts,
                                   st));
     return DPF_OK;
 }
