@@ -10,6 +10,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -59,18 +62,124 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging buffer (hipHostMalloc), grown on demand.
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 struct Dev {
     int id = 0;
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;    // kernels
+    hipStream_t cst = nullptr;   // device -> host copies of the pipelined host-buffer paths
+    hipStream_t hst = nullptr;   // host -> device copies (batched Eval's points)
+    hipEvent_t ev_k[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr}, ev_h[2] = {nullptr, nullptr};
     std::mutex mu;
     DevBuf keys, work, out, xs;
+    HostBuf pin[2];
+};
+
+// Parallel host memcpy for the pinned -> caller-buffer leg of the pipelined
+// copies (one thread reaches ~10 GB/s; PCIe delivers ~50).  A fixed pool of
+// workers takes 2 MiB pieces; the caller works too and waits for the rest.
+class CopyPool {
+   public:
+    static CopyPool& get() {
+        static CopyPool pool;
+        return pool;
+    }
+    void memcpy_par(void* dst, const void* src, size_t n) {
+        constexpr size_t kPiece = (size_t)2 << 20;
+        if (n <= kPiece || workers_.empty()) {
+            memcpy(dst, src, n);
+            return;
+        }
+        Job job{static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n, (n + kPiece - 1) / kPiece};
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            jobs_.push_back(&job);
+        }
+        cv_.notify_all();
+        run(job);
+        // Workers that picked the job leave it (active == 0) before it goes out of scope.
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return job.done.load() == job.npieces && job.active == 0; });
+        jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));
+    }
+
+   private:
+    struct Job {
+        uint8_t* dst;
+        const uint8_t* src;
+        size_t n, npieces;
+        size_t active = 0;   // workers inside run(); guarded by mu_
+        std::atomic<size_t> next{0}, done{0};
+        Job(uint8_t* d, const uint8_t* s, size_t nn, size_t np) : dst(d), src(s), n(nn), npieces(np) {}
+    };
+    // Copy pieces of `job` until none is left.
+    static void run(Job& job) {
+        constexpr size_t kPiece = (size_t)2 << 20;
+        for (size_t i; (i = job.next.fetch_add(1)) < job.npieces;) {
+            const size_t off = i * kPiece, len = std::min(kPiece, job.n - off);
+            memcpy(job.dst + off, job.src + off, len);
+            job.done.fetch_add(1);
+        }
+    }
+    CopyPool() {
+        unsigned hw = std::thread::hardware_concurrency();
+        const unsigned n = std::min(7u, hw > 1 ? hw - 1 : 0u);
+        for (unsigned i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || pending() != nullptr; });
+            if (stop_) return;
+            Job* j = pending();
+            ++j->active;
+            lk.unlock();
+            run(*j);
+            lk.lock();
+            --j->active;
+            done_cv_.notify_all();
+        }
+    }
+    Job* pending() {
+        for (Job* j : jobs_)
+            if (j->next.load() < j->npieces) return j;
+        return nullptr;
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<Job*> jobs_;
+    std::vector<std::thread> workers_;
+    bool stop_ = false;
 };
 
 std::mutex g_mu;
 std::vector<std::unique_ptr<Dev>> g_devs;
-
-// Largest output slab staged in HBM per launch by the host-buffer paths.
-constexpr size_t kMaxSlab = (size_t)1 << 30;
 
 struct DeviceGuard {
     int prev = -1;
@@ -132,71 +241,147 @@ int enqueue_full(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t logN, u
     return DPF_OK;
 }
 
-// Host-buffer EvalFull of keys [0, nk) on one device, output slab-chunked.
+// Pipelined device -> host output of `nchunks` chunks (<= chunk_cap bytes
+// each).  produce(i, dbuf, bytes, host_off) enqueues the kernels writing
+// chunk i into device slot dbuf on d.st.  Kernel i, the PCIe copy of chunk
+// i-1 (d.cst, into a pinned slot) and the host copy of chunk i-2 (pinned ->
+// caller buffer, CopyPool) overlap; two device and two pinned slots.
+constexpr size_t kStageBytes = (size_t)32 << 20;
+
+int ensure_staging(Dev& d, size_t chunk_cap) {
+    if (!d.cst) {
+        HIP_TRY(hipStreamCreateWithFlags(&d.cst, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(hipEventCreateWithFlags(&d.ev_k[i], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&d.ev_c[i], hipEventDisableTiming));
+        }
+    }
+    HIP_TRY(hipError_t(d.out.ensure(2 * chunk_cap)));
+    for (int i = 0; i < 2; ++i) HIP_TRY(d.pin[i].ensure(chunk_cap));
+    return DPF_OK;
+}
+
+template <class Produce>
+int pipeline_d2h(Dev& d, size_t nchunks, size_t chunk_cap, Produce produce, uint8_t* out) {
+    if (nchunks == 0) return DPF_OK;
+    if (int rc = ensure_staging(d, chunk_cap)) return rc;
+    size_t bytes[2] = {0, 0}, off[2] = {0, 0};
+    auto drain = [&](size_t i) -> int {              // chunk i: wait for its PCIe copy, then host copy
+        const int s = (int)(i & 1);
+        HIP_TRY(hipEventSynchronize(d.ev_c[s]));
+        CopyPool::get().memcpy_par(out + off[s], d.pin[s].p, bytes[s]);
+        return DPF_OK;
+    };
+    for (size_t i = 0; i < nchunks; ++i) {
+        const int s = (int)(i & 1);
+        uint8_t* dbuf = (uint8_t*)d.out.p + (size_t)s * chunk_cap;
+        if (i >= 2) HIP_TRY(hipStreamWaitEvent(d.st, d.ev_c[s], 0));   // slot's previous PCIe copy done
+        if (int rc = produce(i, dbuf, bytes[s], off[s])) return rc;
+        HIP_TRY(hipEventRecord(d.ev_k[s], d.st));
+        HIP_TRY(hipStreamWaitEvent(d.cst, d.ev_k[s], 0));
+        HIP_TRY(hipMemcpyAsync(d.pin[s].p, dbuf, bytes[s], hipMemcpyDeviceToHost, d.cst));
+        HIP_TRY(hipEventRecord(d.ev_c[s], d.cst));
+        if (i >= 1)
+            if (int rc = drain(i - 1)) return rc;          // frees pinned slot (i-1)&1 for chunk i+1
+    }
+    return drain(nchunks - 1);
+}
+
+// Host-buffer EvalFull of keys [0, nk) on one device.  Chunks are groups of
+// whole keys, or subtree slabs of one key when its output exceeds a chunk.
 int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t logN, uint8_t* out) {
     std::lock_guard<std::mutex> lk(d.mu);
     DeviceGuard g(d.id);
     const uint32_t stop = stop_of(logN);
     const size_t olen = full_len(logN);
-    if (olen <= kMaxSlab) {
-        const size_t per = std::max<size_t>(1, kMaxSlab / olen);
-        for (size_t k0 = 0; k0 < nk; k0 += per) {
-            const size_t n = std::min(per, nk - k0);
-            HIP_TRY(hipError_t(d.keys.ensure(n * klen)));
-            HIP_TRY(hipError_t(d.work.ensure(n * dpfk::ek_words(stop) * 4)));
-            HIP_TRY(hipError_t(d.out.ensure(n * olen)));
-            HIP_TRY(hipMemcpyAsync(d.keys.p, keys + k0 * klen, n * klen, hipMemcpyHostToDevice, d.st));
-            int rc = enqueue_full((const uint8_t*)d.keys.p, klen, n, logN, 0, 0, (uint8_t*)d.out.p,
-                                  (uint32_t*)d.work.p, d.st);
-            if (rc) return rc;
-            HIP_TRY(hipMemcpyAsync(out + k0 * olen, d.out.p, n * olen, hipMemcpyDeviceToHost, d.st));
-            HIP_TRY(hipStreamSynchronize(d.st));
-        }
+    const size_t ekw = dpfk::ek_words(stop);
+    HIP_TRY(hipError_t(d.keys.ensure(nk * klen)));
+    HIP_TRY(hipError_t(d.work.ensure(nk * ekw * 4)));
+    HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
+    HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, nk, stop, (uint32_t*)d.work.p, d.st));
+    const uint32_t* ek = (const uint32_t*)d.work.p;
+    if (olen <= kStageBytes) {
+        const size_t per = kStageBytes / olen;            // keys per chunk
+        const size_t nch = (nk + per - 1) / per;
+        return pipeline_d2h(d, nch, std::min(per, nk) * olen, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
+            const size_t k0 = i * per, n = std::min(per, nk - k0);
+            HIP_TRY(dpfk::launch_evalfull(ek + k0 * ekw, n, stop, 0, 0, dbuf, olen, d.st));
+            bytes = n * olen;
+            off = k0 * olen;
+            return DPF_OK;
+        }, out);
+    }
+    uint32_t pb = 0;                                      // one key's output exceeds a chunk: subtree slabs
+    while ((olen >> pb) > kStageBytes) ++pb;
+    const size_t slab = olen >> pb, per_key = (size_t)1 << pb;
+    return pipeline_d2h(d, nk * per_key, slab, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
+        const size_t k = i / per_key, p = i % per_key;
+        HIP_TRY(dpfk::launch_evalfull(ek + k * ekw, 1, stop, pb, p, dbuf, slab, d.st));
+        bytes = slab;
+        off = k * olen + p * slab;
         return DPF_OK;
-    }
-    // One key's output exceeds a slab: walk it subtree by subtree.
-    uint32_t pb = 0;
-    while ((olen >> pb) > kMaxSlab) ++pb;
-    const size_t slab = olen >> pb;
-    HIP_TRY(hipError_t(d.keys.ensure(klen)));
-    HIP_TRY(hipError_t(d.work.ensure(dpfk::ek_words(stop) * 4)));
-    HIP_TRY(hipError_t(d.out.ensure(slab)));
-    for (size_t k = 0; k < nk; ++k) {
-        HIP_TRY(hipMemcpyAsync(d.keys.p, keys + k * klen, klen, hipMemcpyHostToDevice, d.st));
-        for (uint64_t p = 0; p < (1ull << pb); ++p) {
-            int rc = enqueue_full((const uint8_t*)d.keys.p, klen, 1, logN, pb, p, (uint8_t*)d.out.p,
-                                  (uint32_t*)d.work.p, d.st);
-            if (rc) return rc;
-            HIP_TRY(hipMemcpyAsync(out + k * olen + p * slab, d.out.p, slab, hipMemcpyDeviceToHost, d.st));
-            HIP_TRY(hipStreamSynchronize(d.st));
-        }
-    }
-    return DPF_OK;
+    }, out);
 }
 
 size_t pir_ek_bytes(size_t nkeys, uint32_t logN);
 size_t eval_work_bytes(size_t nkeys, size_t ppk, uint32_t logN);
 
+// Host-buffer batched Eval on one device, pipelined over chunks of keys:
+// caller xs -> pinned (CopyPool) -> HBM (d.hst) -> k_eval (d.st) -> pinned
+// (d.cst) -> caller out, two slots per stage, so chunk i's kernel overlaps
+// the PCIe copies of its neighbours.
 int eval_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, const uint64_t* xs, size_t ppk,
                    uint32_t logN, uint8_t* out) {
     std::lock_guard<std::mutex> lk(d.mu);
     DeviceGuard g(d.id);
     const uint32_t stop = stop_of(logN);
-    const size_t nq = nk * ppk;
-    HIP_TRY(hipError_t(d.keys.ensure(std::max<size_t>(1, nk * klen))));
-    const size_t wbytes = eval_work_bytes(nk, ppk, logN);
-    HIP_TRY(hipError_t(d.work.ensure(std::max<size_t>(16, wbytes))));
-    HIP_TRY(hipError_t(d.xs.ensure(std::max<size_t>(8, nq * 8))));
-    HIP_TRY(hipError_t(d.out.ensure(std::max<size_t>(1, nq))));
-    HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
-    HIP_TRY(hipMemcpyAsync(d.xs.p, xs, nq * 8, hipMemcpyHostToDevice, d.st));
-    HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, nk, stop, (uint32_t*)d.work.p, d.st));
+    const size_t ekw = dpfk::ek_words(stop);
+    const size_t per = std::max<size_t>(1, std::min(nk, kStageBytes / (ppk * 8)));   // keys per chunk
+    const size_t nch = (nk + per - 1) / per;
     const size_t ekb = pir_ek_bytes(nk, logN);
-    HIP_TRY(dpfk::launch_eval((const uint32_t*)d.work.p, stop, logN, (const uint64_t*)d.xs.p, nq, ppk,
-                              (uint8_t*)d.out.p, (uint8_t*)d.work.p + ekb, wbytes - ekb, d.st));
-    HIP_TRY(hipMemcpyAsync(out, d.out.p, nq, hipMemcpyDeviceToHost, d.st));
-    HIP_TRY(hipStreamSynchronize(d.st));
-    return DPF_OK;
+    const size_t fbytes = dpfk::eval_frontier_bytes(per, stop, ppk);
+    const size_t qcap = per * ppk;                        // queries per chunk
+    HIP_TRY(hipError_t(d.keys.ensure(std::max<size_t>(1, nk * klen))));
+    HIP_TRY(hipError_t(d.work.ensure(std::max<size_t>(16, ekb + fbytes))));
+    HIP_TRY(hipError_t(d.xs.ensure(2 * qcap * 8)));
+    if (int rc = ensure_staging(d, qcap)) return rc;      // d.out: 2 x qcap result bytes
+    for (int i = 0; i < 2; ++i) HIP_TRY(d.pin[i].ensure(qcap * 9));   // [xs qcap*8][results qcap]
+    if (!d.hst) {
+        HIP_TRY(hipStreamCreateWithFlags(&d.hst, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&d.ev_h[i], hipEventDisableTiming));
+    }
+    HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
+    HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, nk, stop, (uint32_t*)d.work.p, d.st));
+    const uint32_t* ek = (const uint32_t*)d.work.p;
+    void* frontier = (uint8_t*)d.work.p + ekb;
+    auto drain = [&](size_t i) -> int {
+        const int s = (int)(i & 1);
+        const size_t k0 = i * per, q = std::min(per, nk - k0) * ppk;
+        HIP_TRY(hipEventSynchronize(d.ev_c[s]));
+        CopyPool::get().memcpy_par(out + k0 * ppk, (uint8_t*)d.pin[s].p + qcap * 8, q);
+        return DPF_OK;
+    };
+    for (size_t i = 0; i < nch; ++i) {
+        const int s = (int)(i & 1);
+        const size_t k0 = i * per, n = std::min(per, nk - k0), q = n * ppk;
+        uint8_t* pin = (uint8_t*)d.pin[s].p;
+        uint64_t* dxs = (uint64_t*)d.xs.p + (size_t)s * qcap;
+        uint8_t* dout = (uint8_t*)d.out.p + (size_t)s * qcap;
+        CopyPool::get().memcpy_par(pin, xs + k0 * ppk, q * 8);
+        if (i >= 2) HIP_TRY(hipStreamWaitEvent(d.hst, d.ev_k[s], 0));   // slot's previous kernel read its xs
+        HIP_TRY(hipMemcpyAsync(dxs, pin, q * 8, hipMemcpyHostToDevice, d.hst));
+        HIP_TRY(hipEventRecord(d.ev_h[s], d.hst));
+        HIP_TRY(hipStreamWaitEvent(d.st, d.ev_h[s], 0));
+        if (i >= 2) HIP_TRY(hipStreamWaitEvent(d.st, d.ev_c[s], 0));    // slot's previous results copied out
+        HIP_TRY(dpfk::launch_eval(ek + k0 * ekw, stop, logN, dxs, q, ppk, dout, frontier, fbytes, d.st));
+        HIP_TRY(hipEventRecord(d.ev_k[s], d.st));
+        HIP_TRY(hipStreamWaitEvent(d.cst, d.ev_k[s], 0));
+        HIP_TRY(hipMemcpyAsync(pin + qcap * 8, dout, q, hipMemcpyDeviceToHost, d.cst));
+        HIP_TRY(hipEventRecord(d.ev_c[s], d.cst));
+        if (i >= 1)
+            if (int rc = drain(i - 1)) return rc;
+    }
+    return drain(nch - 1);
 }
 
 // Run fn(device_index, lo, hi) over `n` items split evenly across g devices.
@@ -259,6 +444,18 @@ void dpf_gpu_shutdown(void) {
         d->work.release();
         d->out.release();
         d->xs.release();
+        for (int i = 0; i < 2; ++i) {
+            d->pin[i].release();
+            if (d->ev_k[i]) (void)hipEventDestroy(d->ev_k[i]);
+            if (d->ev_c[i]) (void)hipEventDestroy(d->ev_c[i]);
+        }
+        for (int i = 0; i < 2; ++i)
+            if (d->ev_h[i]) (void)hipEventDestroy(d->ev_h[i]);
+        for (hipStream_t* t : {&d->cst, &d->hst})
+            if (*t) {
+                (void)hipStreamSynchronize(*t);
+                (void)hipStreamDestroy(*t);
+            }
         (void)hipStreamDestroy(d->st);
     }
     g_devs.clear();
@@ -335,14 +532,19 @@ int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* 
         DeviceGuard gd(d.id);
         HIP_TRY(hipError_t(d.keys.ensure(klen)));
         HIP_TRY(hipError_t(d.work.ensure(dpfk::ek_words(stop) * 4)));
-        HIP_TRY(hipError_t(d.out.ensure(slab)));
         HIP_TRY(hipMemcpyAsync(d.keys.p, key, klen, hipMemcpyHostToDevice, d.st));
-        int rc = enqueue_full((const uint8_t*)d.keys.p, klen, 1, logN, pb, lo, (uint8_t*)d.out.p,
-                              (uint32_t*)d.work.p, d.st);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(out + lo * slab, d.out.p, slab, hipMemcpyDeviceToHost, d.st));
-        HIP_TRY(hipStreamSynchronize(d.st));
-        return DPF_OK;
+        HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, 1, stop, (uint32_t*)d.work.p, d.st));
+        // This device's subtree (pb, lo), streamed out in sub-slabs (pb + extra, lo * 2^extra + j).
+        uint32_t extra = 0;
+        while ((slab >> extra) > kStageBytes && pb + extra < stop) ++extra;
+        const size_t sub = slab >> extra;
+        return pipeline_d2h(d, (size_t)1 << extra, sub, [&](size_t j, uint8_t* dbuf, size_t& bytes, size_t& off) {
+            HIP_TRY(dpfk::launch_evalfull((const uint32_t*)d.work.p, 1, stop, pb + extra, ((uint64_t)lo << extra) + j,
+                                          dbuf, sub, d.st));
+            bytes = sub;
+            off = lo * slab + j * sub;
+            return DPF_OK;
+        }, out);
     });
 }
 

@@ -200,31 +200,40 @@ def EvalFull(key: bytes, logN: int) -> bytes:
     return out.tobytes()
 
 
-def evalfull_batch(keys: np.ndarray, logN: int, ngpus: int = 0) -> np.ndarray:
-    """keys[n, klen] uint8 -> out[n, evalfull_len(logN)] uint8."""
+def evalfull_batch(keys: np.ndarray, logN: int, ngpus: int = 0, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """keys[n, klen] uint8 -> out[n, evalfull_len(logN)] uint8 (written into `out` when given)."""
     kk = np.ascontiguousarray(keys, dtype=np.uint8)
     n, kl = kk.shape
-    out = np.zeros((n, evalfull_len(logN)), np.uint8)
+    if out is None:
+        out = np.empty((n, evalfull_len(logN)), np.uint8)
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.shape == (n, evalfull_len(logN))
     _check(lib().dpf_evalfull_batch(_buf(kk), kl, n, logN, _buf(out), ngpus))
     return out
 
 
-def eval_batch(keys: np.ndarray, xs: np.ndarray, logN: int, ngpus: int = 0) -> np.ndarray:
-    """keys[n, klen], xs[n, p] uint64 -> out[n, p] uint8 (0/1)."""
+def eval_batch(keys: np.ndarray, xs: np.ndarray, logN: int, ngpus: int = 0,
+               out: Optional[np.ndarray] = None) -> np.ndarray:
+    """keys[n, klen], xs[n, p] uint64 -> out[n, p] uint8 (0/1), written into `out` when given."""
     kk = np.ascontiguousarray(keys, dtype=np.uint8)
     x = np.ascontiguousarray(xs, dtype=np.uint64)
     n, kl = kk.shape
     p = x.shape[1]
-    out = np.zeros((n, p), np.uint8)
+    if out is None:
+        out = np.empty((n, p), np.uint8)
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.shape == (n, p)
     _check(lib().dpf_eval_batch(_buf(kk), kl, n, x.ctypes.data_as(_u64p), p, logN, _buf(out), ngpus))
     return out
 
 
-def evalfull_split(key: bytes, logN: int, ngpus: int) -> bytes:
+def evalfull_split(key: bytes, logN: int, ngpus: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """One EvalFull split by top-level subtree over ngpus devices -> uint8
+    array of evalfull_len(logN) bytes (written into `out` when given)."""
     kk = _as_u8(key)
-    out = np.zeros(evalfull_len(logN), np.uint8)
+    if out is None:
+        out = np.empty(evalfull_len(logN), np.uint8)
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size == evalfull_len(logN)
     _check(lib().dpf_evalfull_split(_buf(kk), kk.size, logN, _buf(out), ngpus))
-    return out.tobytes()
+    return out
 
 
 # --------------------------------------------- device-resident (torch) ---

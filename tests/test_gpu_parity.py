@@ -165,7 +165,7 @@ def test_split_single_gpu_matches():
     logN = 18
     _, ka, _ = _keys(1, logN, first=4242)
     full = dpf.EvalFull(ka[0].tobytes(), logN)
-    assert dpf.evalfull_split(ka[0].tobytes(), logN, 1) == full
+    assert dpf.evalfull_split(ka[0].tobytes(), logN, 1).tobytes() == full
     assert full == oracle.evalfull(ka[0].tobytes(), logN, aesni=True)
 
 
