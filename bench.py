@@ -35,9 +35,17 @@ import numpy as np  # noqa: E402
 
 # Per-unit algorithmic figures.
 GATES_PER_AES = 22928          # 2-input gate-equivalents per AES-128-MMO block
-# Override of the measured v_bitop3_b32 rate (Tops), else profiles/r01_valu_peak.json.
-VALU_PEAK_TOPS = float(os.environ.get("DPF_VALU_PEAK_TOPS", "0") or 0) or None
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (spec)
+LOOKUPS_PER_AES = 160          # T-table back end: 16 LDS lookups per round x 10 rounds
+# Peaks from /opt/skills/guides/MI355X_MICROARCH.md (chip parameters):
+#   VALU issue: 256 CU x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz = 78.64 T lane-ops/s;
+#   a v_bitop3_b32 lane-op evaluates 32 bit-lanes x up to 2 two-input gates
+#   -> 5033 T gate-eq/s, the PRG roofline's denominator;
+#   LDS: ds_read_b32 aggregate ~75 TB/s -> 18.75 T 4-byte lookups/s;
+#   HBM: 8 TB/s (spec).
+GUIDE_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+GUIDE_GATE_PEAK_T = GUIDE_VALU_TOPS * 32 * 2
+GUIDE_LDS_LOOKUPS_T = 75e12 / 4 / 1e12
+HBM_PEAK_GBS = 8000.0
 METRIC = "DPF leaf points/sec (EvalFull logN=20, batched keys) + AES blocks/sec"
 
 
@@ -51,79 +59,139 @@ def aes_full(logN: int) -> int:
 
 
 def load_peaks() -> dict:
-    """Measured MI355X rates (tools/valu_peak.hip -> profiles/r01_valu_peak.json)."""
+    """Microbenchmarked MI355X rates (tools/valu_peak.hip ->
+    profiles/r01_valu_peak.json); reported beside the guide's peaks."""
     p = os.path.join(ROOT, "profiles", "r01_valu_peak.json")
     try:
         with open(p) as f:
             d = json.load(f)
     except Exception:
         d = {}
-    return {"bitop3_Tops": float(VALU_PEAK_TOPS or d.get("v_bitop3_b32_Tops", 59.7)),
+    return {"bitop3_Tops": float(d.get("v_bitop3_b32_Tops", 59.7)),
             "lds_lookups_Gs": float(d.get("ds_read_b32_lookup_G_per_s", 16438.3))}
 
 
-def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float) -> dict:
+def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, aes_impl: str = "lds-ttable") -> dict:
     """PRG roofline: 22,928 two-input gate-equivalents per
-    AES-MMO block; ceiling = measured v_bitop3_b32 lane-op rate x 32 bit-lanes
-    x 2 gates per bitop3 (the stricter, bitop3 denominator)."""
+    AES-MMO block against the guide's VALU issue rate x 32 bit-lanes x 2
+    gates per v_bitop3 (5.03 P gate-eq/s).  `lds` is the T-table back end's
+    own ceiling: 160 ds_read_b32 lookups per block against the guide's
+    ~75 TB/s of ds_read_b32 (18.75 T lookups/s)."""
     peaks = load_peaks()
     achieved = aes_rate * GATES_PER_AES / 1e12
-    peak = peaks["bitop3_Tops"] * 32 * 2
     gbs = hbm_bytes / (k_ms * 1e-3) / 1e9
     r = {
         "bound": "valu",
         "achieved": round(achieved, 1),
-        "peak": round(peak, 1),
+        "peak": round(GUIDE_GATE_PEAK_T, 1),
         "unit": "Tgate/s (2-input gate-equivalents; 22,928 per AES-128-MMO block)",
-        "frac": round(achieved / peak, 4),
+        "frac": round(achieved / GUIDE_GATE_PEAK_T, 4),
         "traffic": None,
+        "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.64 T lane-op/s x 32 x 2",
+        "peak_measured": round(peaks["bitop3_Tops"] * 64, 1),
+        "frac_vs_measured": round(achieved / (peaks["bitop3_Tops"] * 64), 4),
         "kernel": kernel,
         "kernel_ms": round(k_ms, 4),
+        "aes_impl": aes_impl,
         "aes_blocks_per_s": aes_rate,
-        "lds_lookup_frac": round(aes_rate * 160 / (peaks["lds_lookups_Gs"] * 1e9), 4),
         "hbm_GBs": round(gbs, 1),
         "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
     }
+    if aes_impl == "lds-ttable":
+        lk = aes_rate * LOOKUPS_PER_AES / 1e12
+        r["lds"] = {"bound": "lds", "achieved": round(lk, 3), "peak": GUIDE_LDS_LOOKUPS_T,
+                    "unit": "T lookups/s (ds_read_b32, 160 per AES-MMO block)",
+                    "frac": round(lk / GUIDE_LDS_LOOKUPS_T, 4),
+                    "peak_measured": round(peaks["lds_lookups_Gs"] / 1e3, 3)}
     # Measured HBM bytes per launch of this kernel from the committed PMC
-    # passes (tools/counters.sh + tools/traffic.py -> profiles/r01_traffic.json).
-    try:
-        with open(os.path.join(ROOT, "profiles", "r01_traffic.json")) as f:
-            t = json.load(f)
-        key = kernel
-        if key in t:
-            r["traffic"] = round(t[key]["traffic_bytes"])
-            r["traffic_over_algorithmic"] = round(t[key]["traffic_bytes"] / hbm_bytes, 3)
-    except Exception:
-        pass
+    # passes (tools/counters.sh + tools/traffic.py -> profiles/*traffic.json).
+    for name in ("r02_traffic.json", "r01_traffic.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                t = json.load(f)
+        except Exception:
+            continue
+        if kernel in t:
+            r["traffic"] = round(t[kernel]["traffic_bytes"])
+            r["traffic_over_algorithmic"] = round(t[kernel]["traffic_bytes"] / hbm_bytes, 3)
+            r["traffic_source"] = f"profiles/{name}"
+            break
     return r
 
 
+def host_cpus() -> dict:
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU
+    quota when one is set (the GPU box gives one GPU's job a CPU share)."""
+    try:
+        mask = len(os.sched_getaffinity(0))
+    except Exception:
+        mask = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    use = min(mask, quota) if quota else mask
+    return {"nproc": os.cpu_count(), "affinity": mask, "cgroup_quota": quota, "model": model, "use": use}
+
+
 def cpu_baseline(logN: int, target_s: float = 10.0) -> dict:
-    """Oracle (reference-faithful C restatement: AES-NI, one block per call,
-    DFS, dpf.go:213-262) on this host's cores, over a bounded sample: passes
-    over one fixed set of keys until about target_s seconds have elapsed."""
+    """The oracle's reference-faithful C restatement (AES-NI, one aes128MMO
+    per call, DFS like evalFullRecursive, dpf.go:213-262) on this host:
+      - configs[0]: single-key EvalFull at logN on ONE core (dpf_test.go:7-21
+        / dpf_main.go:25-30 shape), repeated for ~15% of target_s;
+      - batched: one key per thread at a time over every usable CPU (as
+        parallel goroutines would), passes over a fixed key set for the rest."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from dpf import synth
     import dpf
 
-    cores = min(16, os.cpu_count() or 1)
-    n = cores * 16
+    cpus = host_cpus()
+    cores = cpus["use"]
+    n = cores * 8
     al, s0, s1 = synth.key_seeds(n, logN)
     ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    # configs[0]: one key, one core
+    oracle.evalfull_batch(ka[:1], logN, nthreads=1, aesni=True)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.evalfull_batch(ka[:1], logN, nthreads=1, aesni=True)
+        reps += 1
+        dt1 = time.perf_counter() - t0
+        if dt1 >= 0.15 * target_s:
+            break
+    single_ms = dt1 / reps * 1e3
     oracle.evalfull_batch(ka[:cores], logN, nthreads=cores, aesni=True)   # warm
     passes, t0 = 0, time.perf_counter()
     while True:
         oracle.evalfull_batch(ka, logN, nthreads=cores, aesni=True)
         passes += 1
         dt = time.perf_counter() - t0
-        if dt >= target_s:
+        if dt >= 0.85 * target_s:
             break
     keys = n * passes
     pts = keys * (1 << logN)
     return {"value": pts / dt, "unit": "points/s", "cores": cores, "kind": "port",
             "aes_blocks_per_s": keys * aes_full(logN) / dt,
-            "sample": f"{keys} key-EvalFulls at logN={logN} ({passes} passes over {n} keys, {dt:.1f} s, "
+            "cpu_model": cpus["model"], "nproc": cpus["nproc"], "affinity_cpus": cpus["affinity"],
+            "cgroup_cpu_quota": cpus["cgroup_quota"],
+            "config0_single_key_1core": {"logN": logN, "ms_per_evalfull": round(single_ms, 3),
+                                         "points_per_s": (1 << logN) / (single_ms * 1e-3),
+                                         "aes_blocks_per_s": aes_full(logN) / (single_ms * 1e-3),
+                                         "reps": reps},
+            "sample": f"configs[0]: {reps} single-key EvalFulls at logN={logN} on 1 core ({dt1:.1f} s); "
+                      f"batched: {keys} key-EvalFulls ({passes} passes over {n} keys, {dt:.1f} s, "
                       f"{cores} threads, AES-NI one block per call; oracle/dpf_oracle.c)"}
 
 
@@ -136,10 +204,13 @@ class Ctx:
         self.args = args
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        # One rank per GPU.  DPF_BENCH_BACKEND=gloo plus ranks folded onto the
-        # visible devices lets the multi-rank path run on a 1-GPU box (test only).
-        self.backend = os.environ.get("DPF_BENCH_BACKEND", "nccl")
-        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        # One rank per GPU over RCCL.  When there are more ranks than visible
+        # GPUs (a rehearsal on a 1-GPU box) ranks fold onto the devices and
+        # the control-plane collectives go over gloo (RCCL refuses two ranks
+        # on one GPU).  DPF_BENCH_BACKEND overrides.
+        ndev = max(1, torch.cuda.device_count())
+        self.backend = os.environ.get("DPF_BENCH_BACKEND", "nccl" if self.world <= ndev else "gloo")
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) % ndev
         if self.world > 1:
             torch.cuda.set_device(self.local)
             if self.backend == "nccl":
@@ -148,7 +219,7 @@ class Ctx:
                 dist.init_process_group(self.backend)
         self.dev = torch.device("cuda", self.local)
         torch.cuda.set_device(self.dev)
-        dpf.gpu_init(0)
+        dpf.gpu_init_devices([self.local])      # this rank's GPU only: no context on the others
         self.stream = torch.cuda.current_stream(self.dev)
 
     def timed(self, step, steps, warmup):
@@ -307,7 +378,7 @@ def wl_split(c: Ctx) -> dict:
                                       + " (BASELINE configs[3])",
                                                 "logN": logN, "parallelism": f"subtree-split x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7,false>", k_ms, part)
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7, false, false>", k_ms, part)
     return line
 
 
@@ -364,6 +435,44 @@ def wl_pir(c: Ctx) -> dict:
     return line
 
 
+def spawn_ranks(n: int) -> int:
+    """`python bench.py --gpus N` outside a launcher: start N ranks through
+    torch.distributed.run as a CHILD process (nothing here has touched a GPU)
+    and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args) -> None:
+    """The rank/launch/timing skeleton of a real run without a device: gloo
+    barrier around a no-op step, max-over-ranks time, one line from rank 0."""
+    import torch
+    import torch.distributed as dist
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    t = torch.tensor([time.perf_counter() - t0 + rank * 1e-6], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "max_rank_s": float(t.item()), "local_ranks": os.environ.get("LOCAL_WORLD_SIZE")}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -380,14 +489,25 @@ def main() -> None:
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="split/pir on 1 GPU: time rank 0's share of a W-way split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--check", action="store_true", help="verify a sample of outputs against the oracle")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/collective plumbing only (gloo, no GPU): what the CPU tests run")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and world > 1:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    if args.dry_run:
+        dry_run(args)
+        return
     c = Ctx(args)
     line = {"evalfull": wl_evalfull, "eval": wl_eval, "split": wl_split, "pir": wl_pir}[args.workload](c)
     if c.rank == 0:
-        if args.workload == "evalfull" and not args.no_cpu_baseline:
+        if args.workload == "evalfull" and not args.no_cpu_baseline and c.world == 1:
             line["cpu_baseline"] = cpu_baseline(args.logN, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if c.world > 1:

@@ -104,42 +104,13 @@ __device__ __forceinline__ void aes_round(const uint8_t* tab, uint32_t lo, const
     s.c0 = n0; s.c1 = n1; s.c2 = n2; s.c3 = n3;
 }
 
-#ifndef DPF_LAST_L1
-#define DPF_LAST_L1 0
-#endif
-#if DPF_LAST_L1
-// Last-round S-box through the vector-memory path (L1), beside the LDS
-// T-table: buffer_load_ubyte idxen from a 256-B global table takes 16 of the
-// 160 lookups per block off the LDS pipe (tools/l1_lookup.hip).
-static __constant__ dpfc::Bytes256 c_sbox = dpfc::kSbox;
-__device__ uint8_t sbox_load8(__amdgpu_buffer_rsrc_t r, int vindex, int voffset, int soffset, int aux) __asm(
-    "llvm.amdgcn.struct.ptr.buffer.load.i8");
-template <int K>
-__device__ __forceinline__ uint32_t sbox_l1(uint32_t x) {
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(c_sbox.v), (short)1, 256, 0x00020000);
-    uint32_t i;
-    if constexpr (K == 0) i = x & 0xffu;
-    else if constexpr (K == 3) i = x >> 24;
-    else i = __builtin_amdgcn_perm(x, 0u, 0x0c0c0c00u | (4u + K));
-    return sbox_load8(r, (int)i, 0, 0, 0);
-}
-#endif
-
 // Final round: SubBytes via byte 1 of Te0 (= S[x]), ShiftRows, AddRoundKey.
 template <class K>
 __device__ __forceinline__ void aes_last(const uint8_t* tab, uint32_t lo, const K& k, Blk& s) {
     auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t rk) {
-#if DPF_LAST_L1
-        (void)tab;
-        (void)lo;
-        uint32_t p = __builtin_amdgcn_perm(sbox_l1<1>(b), sbox_l1<0>(a), 0x0c0c0400u);   // {S a.b0, S b.b1, 0, 0}
-        uint32_t q = __builtin_amdgcn_perm(sbox_l1<3>(d), sbox_l1<2>(c), 0x04000c0cu);   // {0, 0, S c.b2, S d.b3}
-#else
         uint32_t la = tl<0>(tab, a, lo), lb = tl<1>(tab, b, lo), lc = tl<2>(tab, c, lo), ld = tl<3>(tab, d, lo);
         uint32_t p = __builtin_amdgcn_perm(lb, la, 0x0c0c0501u);   // {la.b1, lb.b1, 0, 0}
         uint32_t q = __builtin_amdgcn_perm(ld, lc, 0x05010c0cu);   // {0, 0, lc.b1, ld.b1}
-#endif
         return __builtin_amdgcn_bitop3_b32(p, q, rk, kOrXor);
     };
     uint32_t n0 = col(s.c0, s.c1, s.c2, s.c3, k.template get<40>());

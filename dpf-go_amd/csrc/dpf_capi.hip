@@ -91,6 +91,7 @@ struct Dev {
     std::mutex mu;
     DevBuf keys, work, out, xs;
     HostBuf pin[2];
+    ~Dev();
 };
 
 // Parallel host memcpy for the pinned -> caller-buffer leg of the pipelined
@@ -178,8 +179,12 @@ class CopyPool {
     bool stop_ = false;
 };
 
+// Open devices.  Entry points take a snapshot (shared_ptr copies) under
+// g_mu, so dpf_gpu_shutdown only drops the registry's references: a call in
+// flight, or a PIR handle, keeps its devices alive until it is done with
+// them, and the last reference releases the device's buffers and streams.
 std::mutex g_mu;
-std::vector<std::unique_ptr<Dev>> g_devs;
+std::vector<std::shared_ptr<Dev>> g_devs;
 
 struct DeviceGuard {
     int prev = -1;
@@ -192,6 +197,56 @@ struct DeviceGuard {
     }
 };
 
+Dev::~Dev() {
+    std::lock_guard<std::mutex> dl(mu);
+    DeviceGuard g(id);
+    for (hipStream_t t : {st, cst, hst})
+        if (t) (void)hipStreamSynchronize(t);
+    keys.release();
+    work.release();
+    out.release();
+    xs.release();
+    for (int i = 0; i < 2; ++i) {
+        pin[i].release();
+        for (hipEvent_t e : {ev_k[i], ev_c[i], ev_h[i]})
+            if (e) (void)hipEventDestroy(e);
+    }
+    for (hipStream_t t : {st, cst, hst})
+        if (t) (void)hipStreamDestroy(t);
+}
+
+using DevList = std::vector<std::shared_ptr<Dev>>;
+
+int check_gfx950(int ordinal) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ordinal) != hipSuccess) return fail(DPF_ERR_NODEV, "dpf: device query failed");
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(DPF_ERR_NODEV, std::string("dpf: device is ") + prop.gcnArchName + ", need gfx950");
+    return DPF_OK;
+}
+
+// Open exactly the HIP ordinals `ids` (caller holds g_mu, registry empty).
+int open_list(const std::vector<int>& ids) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return fail(DPF_ERR_NODEV, "dpf: no HIP device visible (gfx950 required)");
+    for (int id : ids) {
+        if (id < 0 || id >= n) return fail(DPF_ERR_PARAM, "dpf: device ordinal out of range");
+        if (int rc = check_gfx950(id)) return rc;
+    }
+    DevList devs;
+    for (int id : ids) {
+        auto d = std::make_shared<Dev>();
+        d->id = id;
+        DeviceGuard g(id);
+        if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess)
+            return fail(DPF_ERR_HIP, "dpf: hipStreamCreate failed");
+        devs.push_back(std::move(d));
+    }
+    g_devs = std::move(devs);
+    return (int)g_devs.size();
+}
+
 int open_devices(int ngpus) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_devs.empty()) return (int)g_devs.size();
@@ -199,34 +254,33 @@ int open_devices(int ngpus) {
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0) return fail(DPF_ERR_NODEV, "dpf: no HIP device visible (gfx950 required)");
     if (ngpus > 0) n = std::min(n, ngpus);
-    for (int i = 0; i < n; ++i) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, i) != hipSuccess) return fail(DPF_ERR_NODEV, "dpf: device query failed");
-        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-            return fail(DPF_ERR_NODEV, std::string("dpf: device is ") + prop.gcnArchName + ", need gfx950");
-    }
-    for (int i = 0; i < n; ++i) {
-        auto d = std::make_unique<Dev>();
-        d->id = i;
-        DeviceGuard g(i);
-        if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess)
-            return fail(DPF_ERR_HIP, "dpf: hipStreamCreate failed");
-        g_devs.push_back(std::move(d));
-    }
-    return n;
+    std::vector<int> ids;
+    for (int i = 0; i < n; ++i) ids.push_back(i);
+    return open_list(ids);
 }
 
-int ensure_open() {
+// The opened devices, opening every visible one on first use.  Returns an
+// empty list (and sets the error) when none can be opened.
+DevList devices(int* rc) {
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        if (!g_devs.empty()) return (int)g_devs.size();
+        if (!g_devs.empty()) {
+            *rc = (int)g_devs.size();
+            return g_devs;
+        }
     }
-    return open_devices(0);
+    *rc = open_devices(0);
+    std::lock_guard<std::mutex> lk(g_mu);
+    return *rc > 0 ? g_devs : DevList{};
 }
 
+// The reference reads k[0:17], the level records k[17+18i : 17+18i+18] for
+// i < stop and the final CW at k[len-16 : len] (dpf.go:175-176,186-188,206,
+// 219,231-233): any key of at least 17 + 18*stop bytes evaluates without an
+// index panic, including keys whose final CW overlaps the last record.
 int check_key(size_t klen, uint32_t logN) {
     if (logN > 63) return fail(DPF_ERR_PARAM, "dpf: logN > 63");
-    if (klen < key_len(logN)) return fail(DPF_ERR_KEYLEN, "dpf: key shorter than 33+18*(logN-7) bytes");
+    if (klen < 17 + 18 * (size_t)stop_of(logN)) return fail(DPF_ERR_KEYLEN, "dpf: key shorter than 17+18*(logN-7) bytes");
     return DPF_OK;
 }
 
@@ -404,10 +458,13 @@ int shard(size_t n, int g, F fn) {
     return DPF_OK;
 }
 
-int pick_ngpus(int ngpus) {
-    int have = ensure_open();
-    if (have <= 0) return have;
-    return ngpus <= 0 ? have : std::min(ngpus, have);
+// The first min(ngpus, opened) devices (ngpus <= 0: all); empty + error set on failure.
+DevList pick_devs(int ngpus, int* rc) {
+    DevList devs = devices(rc);
+    if (*rc <= 0) return {};
+    if (ngpus > 0 && (size_t)ngpus < devs.size()) devs.resize((size_t)ngpus);
+    *rc = (int)devs.size();
+    return devs;
 }
 
 // Expanded keys at the start of a PIR workspace, padded to 256 B.
@@ -434,31 +491,27 @@ size_t dpf_workspace_size(size_t nkeys, uint32_t logN) {
 
 int dpf_gpu_init(int ngpus) { return open_devices(ngpus); }
 
-void dpf_gpu_shutdown(void) {
+int dpf_gpu_init_devices(const int* ordinals, int n) {
+    if (n <= 0 || ordinals == nullptr) return fail(DPF_ERR_PARAM, "dpf: empty device list");
+    std::vector<int> ids(ordinals, ordinals + n);
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto& d : g_devs) {
-        std::lock_guard<std::mutex> dl(d->mu);
-        DeviceGuard g(d->id);
-        (void)hipStreamSynchronize(d->st);
-        d->keys.release();
-        d->work.release();
-        d->out.release();
-        d->xs.release();
-        for (int i = 0; i < 2; ++i) {
-            d->pin[i].release();
-            if (d->ev_k[i]) (void)hipEventDestroy(d->ev_k[i]);
-            if (d->ev_c[i]) (void)hipEventDestroy(d->ev_c[i]);
-        }
-        for (int i = 0; i < 2; ++i)
-            if (d->ev_h[i]) (void)hipEventDestroy(d->ev_h[i]);
-        for (hipStream_t* t : {&d->cst, &d->hst})
-            if (*t) {
-                (void)hipStreamSynchronize(*t);
-                (void)hipStreamDestroy(*t);
-            }
-        (void)hipStreamDestroy(d->st);
+    if (!g_devs.empty()) {
+        bool same = g_devs.size() == ids.size();
+        for (size_t i = 0; same && i < ids.size(); ++i) same = g_devs[i]->id == ids[i];
+        if (!same) return fail(DPF_ERR_PARAM, "dpf: already initialised with other devices (dpf_gpu_shutdown first)");
+        return (int)g_devs.size();
     }
-    g_devs.clear();
+    return open_list(ids);
+}
+
+void dpf_gpu_shutdown(void) {
+    DevList old;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        old.swap(g_devs);
+    }
+    // Dropping the registry's references; a device still used by an
+    // in-flight call or a PIR handle is released when that lets go.
 }
 
 int dpf_gpu_count(void) {
@@ -486,11 +539,12 @@ int dpf_gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s
 int dpf_evalfull_batch(const uint8_t* keys, size_t klen, size_t nkeys, uint32_t logN, uint8_t* out, int ngpus) {
     if (int rc = check_key(klen, logN)) return rc;
     if (nkeys == 0) return DPF_OK;
-    const int g = pick_ngpus(ngpus);
+    int g = 0;
+    const DevList devs = pick_devs(ngpus, &g);
     if (g <= 0) return g;
     const size_t olen = full_len(logN);
     return shard(nkeys, g, [&](int dev, size_t lo, size_t hi) {
-        return full_on_device(*g_devs[(size_t)dev], keys + lo * klen, klen, hi - lo, logN, out + lo * olen);
+        return full_on_device(*devs[(size_t)dev], keys + lo * klen, klen, hi - lo, logN, out + lo * olen);
     });
 }
 
@@ -502,10 +556,11 @@ int dpf_eval_batch(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_
                    uint8_t* out, int ngpus) {
     if (int rc = check_key(klen, logN)) return rc;
     if (nkeys == 0 || ppk == 0) return DPF_OK;
-    const int g = pick_ngpus(ngpus);
+    int g = 0;
+    const DevList devs = pick_devs(ngpus, &g);
     if (g <= 0) return g;
     return shard(nkeys, g, [&](int dev, size_t lo, size_t hi) {
-        return eval_on_device(*g_devs[(size_t)dev], keys + lo * klen, klen, hi - lo, xs + lo * ppk, ppk, logN,
+        return eval_on_device(*devs[(size_t)dev], keys + lo * klen, klen, hi - lo, xs + lo * ppk, ppk, logN,
                               out + lo * ppk);
     });
 }
@@ -516,7 +571,8 @@ int dpf_eval(const uint8_t* key, size_t klen, uint64_t x, uint32_t logN, uint8_t
 
 int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out, int ngpus) {
     if (int rc = check_key(klen, logN)) return rc;
-    const int have = pick_ngpus(ngpus);
+    int have = 0;
+    const DevList devs = pick_devs(0, &have);
     if (have <= 0) return have;
     const uint32_t stop = stop_of(logN);
     const int want = ngpus <= 0 ? have : ngpus;
@@ -527,7 +583,7 @@ int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* 
     const size_t slab = full_len(logN) >> pb;
     return shard((size_t)want, want, [&](int dev, size_t lo, size_t hi) {
         (void)hi;
-        Dev& d = *g_devs[(size_t)dev];
+        Dev& d = *devs[(size_t)dev];
         std::lock_guard<std::mutex> lk(d.mu);
         DeviceGuard gd(d.id);
         HIP_TRY(hipError_t(d.keys.ensure(klen)));
@@ -637,18 +693,28 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     return DPF_OK;
 }
 
+// A PIR handle owns references to the devices its shards live on, so it
+// stays usable (and freeable) after dpf_gpu_shutdown.
 struct PirDb {
     uint32_t logN = 0, pbits = 0;
     uint64_t nrec = 0;
+    DevList devs;                  // per shard: its device
     std::vector<void*> shard;      // per device: its DB slice
     std::vector<uint64_t> shard_n; // records in that slice
+    ~PirDb() {
+        for (size_t i = 0; i < shard.size(); ++i) {
+            DeviceGuard gd(devs[i]->id);
+            (void)hipFree(shard[i]);
+        }
+    }
 };
 
 int dpf_pir_db_create(const uint8_t* db, uint64_t nrec, uint32_t logN, int ngpus, void** handle) {
     if (!handle) return fail(DPF_ERR_PARAM, "dpf: null handle");
     *handle = nullptr;
     if (logN > 63 || (logN < 64 && nrec > (1ull << logN))) return fail(DPF_ERR_PARAM, "dpf: DB larger than 2^logN");
-    const int have = pick_ngpus(ngpus);
+    int have = 0;
+    const DevList devs = pick_devs(0, &have);
     if (have <= 0) return have;
     const int want = ngpus <= 0 ? have : ngpus;
     uint32_t pb = 0;
@@ -663,20 +729,15 @@ int dpf_pir_db_create(const uint8_t* db, uint64_t nrec, uint32_t logN, int ngpus
     for (int g = 0; g < want; ++g) {
         const uint64_t lo = std::min<uint64_t>(nrec, (uint64_t)g * slice);
         const uint64_t hi = std::min<uint64_t>(nrec, lo + slice);
-        DeviceGuard gd(g_devs[(size_t)g]->id);
+        DeviceGuard gd(devs[(size_t)g]->id);
         void* p = nullptr;
         const size_t bytes = std::max<uint64_t>(hi - lo, 1) * 32;
-        if (hipMalloc(&p, bytes) != hipSuccess) {
-            for (void* q : h->shard) (void)hipFree(q);
-            return fail(DPF_ERR_NOMEM, "dpf: DB shard allocation failed");
-        }
-        if (hi > lo && hipMemcpy(p, db + lo * 32, (hi - lo) * 32, hipMemcpyHostToDevice) != hipSuccess) {
-            (void)hipFree(p);
-            for (void* q : h->shard) (void)hipFree(q);
-            return fail(DPF_ERR_HIP, "dpf: DB upload failed");
-        }
+        if (hipMalloc(&p, bytes) != hipSuccess) return fail(DPF_ERR_NOMEM, "dpf: DB shard allocation failed");
+        h->devs.push_back(devs[(size_t)g]);     // ~PirDb frees what was allocated so far
         h->shard.push_back(p);
         h->shard_n.push_back(hi - lo);
+        if (hi > lo && hipMemcpy(p, db + lo * 32, (hi - lo) * 32, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(DPF_ERR_HIP, "dpf: DB upload failed");
     }
     *handle = h.release();
     return DPF_OK;
@@ -690,7 +751,7 @@ int dpf_pir_answer(void* handle, const uint8_t* keys, size_t klen, size_t nkeys,
     std::vector<std::vector<uint8_t>> part((size_t)g, std::vector<uint8_t>(nkeys * 32));
     int rc = shard((size_t)g, g, [&](int dev, size_t lo, size_t hi) {
         (void)hi;
-        Dev& d = *g_devs[(size_t)dev];
+        Dev& d = *h->devs[(size_t)dev];
         std::lock_guard<std::mutex> lk(d.mu);
         DeviceGuard gd(d.id);
         HIP_TRY(hipError_t(d.keys.ensure(std::max<size_t>(1, nkeys * klen))));
@@ -711,14 +772,6 @@ int dpf_pir_answer(void* handle, const uint8_t* keys, size_t klen, size_t nkeys,
     return DPF_OK;
 }
 
-void dpf_pir_db_free(void* handle) {
-    PirDb* h = (PirDb*)handle;
-    if (!h) return;
-    for (size_t i = 0; i < h->shard.size(); ++i) {
-        DeviceGuard gd(g_devs[i]->id);
-        (void)hipFree(h->shard[i]);
-    }
-    delete h;
-}
+void dpf_pir_db_free(void* handle) { delete (PirDb*)handle; }
 
 }  // extern "C"

@@ -47,26 +47,15 @@ __device__ __forceinline__ Blk load_blk(const uint32_t* p) {
 }
 
 // prg (dpf.go:59-69) plus the parent's CW correction (dpf.go:230-238).
-#ifndef DPF_PRG_ILP
-#define DPF_PRG_ILP 0
-#endif
-// The two independent MMOs of a PRG call (or of a leaf pair).  Written as two
-// plain mmo1 calls the scheduler interleaves them freely: 98.9 G blocks/s in
-// tools/aes_variants.hip, against 88.4 for the round-by-round interleave
-// (DPF_PRG_ILP 2) and 93.3 fully serialized (DPF_PRG_ILP 1).
+// The two independent MMOs of a PRG call (or of a leaf pair), written as two
+// plain mmo1 calls so the scheduler interleaves them freely: 98.9 G blocks/s
+// in tools/aes_variants.hip, against 88.4 for a round-by-round interleave
+// and 93.3 fully serialized (r01 A/B, profiles/r01/full_ilp*).
 template <class KA, class KB>
 __device__ __forceinline__ void mmo_pair(const uint8_t* tab, uint32_t lo, const KA& ka, Blk xa, Blk& oa,
                                          const KB& kb, Blk xb, Blk& ob) {
-#if DPF_PRG_ILP == 1
-    oa = mmo1(tab, lo, ka, xa);
-    __builtin_amdgcn_sched_barrier(0);
-    ob = mmo1(tab, lo, kb, xb);
-#elif DPF_PRG_ILP == 2
-    mmo2(tab, lo, ka, xa, oa, kb, xb, ob);
-#else
     oa = mmo1(tab, lo, ka, xa);
     ob = mmo1(tab, lo, kb, xb);
-#endif
 }
 
 __device__ __forceinline__ void expand(const uint8_t* tab, uint32_t lo, const Node& n, const CW& cw, Node& L,
@@ -318,7 +307,7 @@ static uint32_t pick_block(uint64_t n, uint32_t maxb) {
     const uint64_t cus = (uint64_t)cu_count();
     uint32_t b = 64;
     while (b < maxb && n > cus * b) b <<= 1;
-    return b;
+    return b < maxb ? b : maxb;   // maxb need not be a power of two (occ5 variant: 640)
 }
 
 // Per-thread subtree depth D and workgroup size.  A thread walks span - D
@@ -399,7 +388,8 @@ hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, ui
 }
 
 uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key) {
-    // Shared frontier at level L when a key's points cover it: 2^(L+1) <= ppk.
+    // Shared frontier at level L when a key's points cover it twice over:
+    // 2^(L+2) <= ppk, i.e. >= 4 points per frontier node (and L >= 4).
     uint32_t L = 0;
     while (L < kMaxFrontierHbm && L < stop && (2ull << (L + 1)) <= pts_per_key) ++L;
     return L >= 4 ? L : 0;

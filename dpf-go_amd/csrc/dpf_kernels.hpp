@@ -32,7 +32,7 @@ hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, ui
                            uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st);
 
 // Batched Eval.  When a key has enough points to share the top of its tree
-// (2^(L+1) <= pts_per_key), the 2^L nodes at level L of every key are first
+// (2^(L+2) <= pts_per_key), the 2^L nodes at level L of every key are first
 // computed into `frontier` (eval_frontier_bytes of it) and each query starts
 // there; with frontier == nullptr (or too small) every walk starts at the root.
 uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key);

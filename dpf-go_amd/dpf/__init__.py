@@ -57,6 +57,7 @@ SIGNATURES = {
     "dpf_evalfull_len": (_sz, [_u32]),
     "dpf_workspace_size": (_sz, [_sz, _u32]),
     "dpf_gpu_init": (_int, [_int]),
+    "dpf_gpu_init_devices": (_int, [ctypes.POINTER(_int), _int]),
     "dpf_gpu_shutdown": (None, []),
     "dpf_gpu_count": (_int, []),
     "dpf_gen_seeded": (_int, [_u64, _u32, _u8p, _u8p, _u8p, _u8p]),
@@ -136,6 +137,15 @@ def workspace_size(nkeys: int, logN: int) -> int:
 
 def gpu_init(ngpus: int = 0) -> int:
     rc = lib().dpf_gpu_init(ngpus)
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+def gpu_init_devices(ordinals: Sequence[int]) -> int:
+    """Open exactly these HIP ordinals (one process per GPU: its own only)."""
+    ids = (_int * len(ordinals))(*ordinals)
+    rc = lib().dpf_gpu_init_devices(ids, len(ordinals))
     if rc < 0:
         _check(rc)
     return rc

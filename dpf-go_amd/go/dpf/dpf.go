@@ -112,6 +112,13 @@ func EvalBatch(keys []DPFkey, xs [][]uint64, logN uint64, ngpus int) [][]byte {
 		copy(pts[i*ppk:], xs[i])
 	}
 	flat := make([]byte, ppk*len(keys))
+	if ppk == 0 { // no queries: nothing to send (and &pts[0] would not exist)
+		out := make([][]byte, len(keys))
+		for i := range out {
+			out[i] = flat[0:0:0]
+		}
+		return out
+	}
 	check(C.dpf_eval_batch(u8(packed), C.size_t(kl), C.size_t(len(keys)),
 		(*C.uint64_t)(unsafe.Pointer(&pts[0])), C.size_t(ppk), C.uint32_t(logN), u8(flat), C.int(ngpus)))
 	out := make([][]byte, len(keys))

@@ -32,7 +32,7 @@ extern "C" {
 
 #define DPF_OK 0
 #define DPF_ERR_PARAM (-1)   /* invalid alpha/logN: where Gen panics (dpf.go:72-74) */
-#define DPF_ERR_KEYLEN (-2)  /* key shorter than 33+18*stop: where Eval/EvalFull index out of range */
+#define DPF_ERR_KEYLEN (-2)  /* key shorter than 17+18*stop: where Eval/EvalFull index out of range */
 #define DPF_ERR_NODEV (-3)   /* no usable gfx950 device / dpf_gpu_init not possible */
 #define DPF_ERR_HIP (-4)     /* HIP runtime error (message in dpf_last_error) */
 #define DPF_ERR_NOMEM (-5)   /* device or host allocation failed */
@@ -51,8 +51,16 @@ size_t dpf_workspace_size(size_t nkeys, uint32_t logN);
 /* ---- device management (no reference counterpart: the reference has no
  *      device; dpf.go:22-44 init() is the nearest analogue) --------------- */
 /* Open ngpus devices (<= 0: every visible device).  Idempotent.  Returns the
- * number of devices opened (> 0) or a negative error. */
+ * number of devices opened (> 0) or a negative error.  Host-buffer entry
+ * points open every visible device on first use when nothing is open. */
 int dpf_gpu_init(int ngpus);
+/* Open exactly the HIP ordinals ordinals[0..n) (e.g. one process per GPU:
+ * its LOCAL_RANK only), so no context is created on any other device.
+ * Idempotent for the same list; DPF_ERR_PARAM if other devices are open. */
+int dpf_gpu_init_devices(const int* ordinals, int n);
+/* Drops the library's references to the opened devices.  Calls already in
+ * flight and live PIR handles keep the devices they use until they finish
+ * (or are freed); later host-buffer calls re-open devices on demand. */
 void dpf_gpu_shutdown(void);
 int dpf_gpu_count(void);
 
@@ -69,6 +77,9 @@ int dpf_gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s
                          uint8_t* kas, uint8_t* kbs, int nthreads);
 
 /* ---- evaluation, host buffers (synchronous; PCIe-inclusive) ------------ */
+/* Keys: at least 17 + 18*stop bytes (the reference's own index bound,
+ * dpf.go:175-176,186-188); the final CW is always k[len-16 : len]
+ * (dpf.go:206,219), longer keys are accepted.  Shorter: DPF_ERR_KEYLEN. */
 /* Eval (dpf.go:171-211): *out_bit = 0/1. */
 int dpf_eval(const uint8_t* key, size_t key_len, uint64_t x, uint32_t logN, uint8_t* out_bit);
 /* EvalFull (dpf.go:243-262): out = dpf_evalfull_len(logN) bytes. */

@@ -1,0 +1,235 @@
+/*
+ * host_sanity.c — drives the host side of libdpf_hip.so under AddressSanitizer
+ * + UBSan (built by `make -C dpf-go_amd asan`, run by tests/test_capi.py).
+ *
+ * Without a GPU (this container) it covers the host code that runs anyway:
+ * Gen (dpf.go:71-169) single, batched over threads and against the
+ * reference's invariants (shared CW tail, t0 ^ t1 == 1, dpf.go:83-92,166-167),
+ * argument validation (Gen's panic cases, short keys), every evaluation entry
+ * point failing cleanly with DPF_ERR_NODEV, device (re)open/shutdown cycles,
+ * PIR handle create/free, and per-thread dpf_last_error.
+ * With a GPU (argv[1] == "gpu") it also runs concurrent host-buffer
+ * EvalFull / Eval from several threads while another thread shuts the
+ * library down and re-opens it, and frees a PIR handle after shutdown:
+ * the CopyPool, shard() threads, per-device mutexes and the shared_ptr
+ * device registry under the sanitizers.  Exit status 0 = pass.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dpf_hip.h"
+
+#define CHECK(cond, ...)                                   \
+    do {                                                   \
+        if (!(cond)) {                                     \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);                  \
+            fprintf(stderr, " (%s)\n", dpf_last_error());  \
+            exit(1);                                       \
+        }                                                  \
+    } while (0)
+
+static int bit(const uint8_t* b, uint64_t x) { return (b[x >> 3] >> (x & 7)) & 1; }
+
+static void gen_checks(void) {
+    for (uint32_t logN = 0; logN <= 63; logN += 7) {
+        size_t kl = dpf_key_len(logN);
+        uint8_t* ka = malloc(kl);
+        uint8_t* kb = malloc(kl);
+        uint8_t s0[16], s1[16];
+        for (int i = 0; i < 16; ++i) {
+            s0[i] = (uint8_t)(i * 7 + logN);
+            s1[i] = (uint8_t)(i * 13 + 1);
+        }
+        uint64_t alpha = logN == 0 ? 0 : (0x123456789abcdefull & ((logN == 64 ? 0 : (1ull << logN)) - 1));
+        CHECK(dpf_gen_seeded(alpha, logN, s0, s1, ka, kb) == DPF_OK, "gen_seeded logN=%u", logN);
+        CHECK((ka[16] ^ kb[16]) == 1, "t0 ^ t1 != 1");
+        CHECK(memcmp(ka + 17, kb + 17, kl - 17) == 0, "CW tails differ");
+        CHECK((ka[0] & 1) == 0 && (kb[0] & 1) == 0, "root seed LSB not cleared");
+        CHECK(dpf_gen(alpha, logN, ka, kb) == DPF_OK, "gen");
+        free(ka);
+        free(kb);
+    }
+    uint8_t k[64];
+    CHECK(dpf_gen(256, 8, k, k) == DPF_ERR_PARAM, "alpha >= 2^logN accepted");
+    CHECK(dpf_gen(0, 64, k, k) == DPF_ERR_PARAM, "logN 64 accepted");
+
+    /* batched over threads == one by one */
+    const size_t n = 700;
+    const uint32_t logN = 20;
+    size_t kl = dpf_key_len(logN);
+    uint64_t* al = malloc(n * 8);
+    uint8_t* s0 = malloc(n * 16);
+    uint8_t* s1 = malloc(n * 16);
+    uint8_t* ka = malloc(n * kl);
+    uint8_t* kb = malloc(n * kl);
+    uint8_t* one_a = malloc(kl);
+    uint8_t* one_b = malloc(kl);
+    for (size_t i = 0; i < n; ++i) {
+        al[i] = (i * 2654435761u) & ((1u << logN) - 1);
+        for (int j = 0; j < 16; ++j) {
+            s0[16 * i + j] = (uint8_t)(i + 3 * j);
+            s1[16 * i + j] = (uint8_t)(i * 5 + j);
+        }
+    }
+    CHECK(dpf_gen_batch_seeded(al, logN, s0, s1, n, ka, kb, 0) == DPF_OK, "gen_batch");
+    for (size_t i = 0; i < n; i += 37) {
+        CHECK(dpf_gen_seeded(al[i], logN, s0 + 16 * i, s1 + 16 * i, one_a, one_b) == DPF_OK, "gen_seeded");
+        CHECK(memcmp(one_a, ka + i * kl, kl) == 0 && memcmp(one_b, kb + i * kl, kl) == 0, "batch != single");
+    }
+    CHECK(dpf_gen_batch_seeded(al, logN, s0, s1, 0, ka, kb, 3) == DPF_OK, "empty batch");
+    al[5] = 1u << logN;
+    CHECK(dpf_gen_batch_seeded(al, logN, s0, s1, n, ka, kb, 4) == DPF_ERR_PARAM, "bad alpha accepted");
+    free(al); free(s0); free(s1); free(ka); free(kb); free(one_a); free(one_b);
+}
+
+struct eval_job {
+    int id, iters;
+    int rc;
+};
+
+static void* eval_thread(void* p) {
+    struct eval_job* j = p;
+    const uint32_t logN = 14;
+    size_t kl = dpf_key_len(logN), ol = dpf_evalfull_len(logN);
+    const size_t nk = 3;
+    uint8_t* ka = malloc(nk * kl);
+    uint8_t* kb = malloc(nk * kl);
+    uint8_t* fa = malloc(nk * ol);
+    uint8_t* fb = malloc(nk * ol);
+    uint64_t xs[3 * 40];
+    uint8_t ea[3 * 40], eb[3 * 40];
+    j->rc = 0;
+    for (int it = 0; it < j->iters && !j->rc; ++it) {
+        uint64_t alpha[3];
+        for (size_t k = 0; k < nk; ++k) {
+            alpha[k] = (uint64_t)(j->id * 1000 + it * 17 + k * 5000) & ((1u << logN) - 1);
+            if (dpf_gen(alpha[k], logN, ka + k * kl, kb + k * kl)) j->rc = 1;
+            for (int q = 0; q < 40; ++q) xs[k * 40 + q] = q == 7 ? alpha[k] : (uint64_t)(q * 411 + it) & ((1u << logN) - 1);
+        }
+        int r1 = dpf_evalfull_batch(ka, kl, nk, logN, fa, 0);
+        int r2 = dpf_evalfull_batch(kb, kl, nk, logN, fb, 0);
+        int r3 = dpf_eval_batch(ka, kl, nk, xs, 40, logN, ea, 0);
+        int r4 = dpf_eval_batch(kb, kl, nk, xs, 40, logN, eb, 0);
+        if (r1 || r2 || r3 || r4) {
+            fprintf(stderr, "thread %d: rc %d %d %d %d (%s)\n", j->id, r1, r2, r3, r4, dpf_last_error());
+            j->rc = 1;
+            break;
+        }
+        for (size_t k = 0; k < nk; ++k) {
+            for (int q = 0; q < 40; ++q) {
+                uint64_t x = xs[k * 40 + q];
+                int want = x == alpha[k];
+                if ((ea[k * 40 + q] ^ eb[k * 40 + q]) != want) j->rc = 1;
+                if ((bit(fa + k * ol, x) ^ bit(fb + k * ol, x)) != want) j->rc = 1;
+                if (bit(fa + k * ol, x) != ea[k * 40 + q]) j->rc = 1;
+            }
+        }
+    }
+    free(ka); free(kb); free(fa); free(fb);
+    return NULL;
+}
+
+static void* shutdown_thread(void* p) {
+    int n = *(int*)p;
+    for (int i = 0; i < n; ++i) {
+        dpf_gpu_shutdown();
+        (void)dpf_gpu_init(1);
+    }
+    return NULL;
+}
+
+static void gpu_checks(void) {
+    CHECK(dpf_gpu_init(1) >= 1, "no gfx950 device");
+    /* a PIR handle outlives shutdown and is freed afterwards */
+    const uint32_t logN = 10;
+    uint8_t* db = malloc(1024 * 32);
+    for (int i = 0; i < 1024 * 32; ++i) db[i] = (uint8_t)(i * 31 + 7);
+    void* h = NULL;
+    CHECK(dpf_pir_db_create(db, 1024, logN, 1, &h) == DPF_OK && h != NULL, "pir create");
+    size_t kl = dpf_key_len(logN);
+    uint8_t* ka = malloc(kl);
+    uint8_t* kb = malloc(kl);
+    uint8_t aa[32], ab[32];
+    CHECK(dpf_gen(333, logN, ka, kb) == DPF_OK, "gen");
+    dpf_gpu_shutdown();
+    CHECK(dpf_pir_answer(h, ka, kl, 1, aa) == DPF_OK && dpf_pir_answer(h, kb, kl, 1, ab) == DPF_OK, "answer");
+    for (int i = 0; i < 32; ++i) CHECK((aa[i] ^ ab[i]) == db[333 * 32 + i], "PIR after shutdown");
+    dpf_pir_db_free(h);
+    free(ka); free(kb); free(db);
+
+    /* concurrent evaluation racing shutdown / re-open */
+    enum { NT = 4 };
+    pthread_t th[NT], sd;
+    struct eval_job jobs[NT];
+    int cycles = 5;
+    for (int i = 0; i < NT; ++i) {
+        jobs[i].id = i;
+        jobs[i].iters = 6;
+        pthread_create(&th[i], NULL, eval_thread, &jobs[i]);
+    }
+    pthread_create(&sd, NULL, shutdown_thread, &cycles);
+    for (int i = 0; i < NT; ++i) pthread_join(th[i], NULL);
+    pthread_join(sd, NULL);
+    for (int i = 0; i < NT; ++i) CHECK(jobs[i].rc == 0, "thread %d failed", i);
+    /* a large host-buffer EvalFull goes through the CopyPool (> 2 MiB) */
+    {
+        const uint32_t L = 24;
+        size_t kl2 = dpf_key_len(L), ol2 = dpf_evalfull_len(L);
+        uint8_t* k2a = malloc(kl2);
+        uint8_t* k2b = malloc(kl2);
+        uint8_t* o = malloc(2 * ol2);
+        CHECK(dpf_gen(0xABCDE, L, k2a, k2b) == DPF_OK, "gen24");
+        CHECK(dpf_evalfull(k2a, kl2, L, o) == DPF_OK && dpf_evalfull(k2b, kl2, L, o + ol2) == DPF_OK, "full24");
+        size_t ones = 0;
+        for (size_t i = 0; i < ol2; ++i) ones += __builtin_popcount(o[i] ^ o[ol2 + i]);
+        CHECK(ones == 1 && bit(o, 0xABCDE) != bit(o + ol2, 0xABCDE), "point function at logN=24");
+        free(k2a); free(k2b); free(o);
+    }
+    dpf_gpu_shutdown();
+}
+
+static void nodev_checks(void) {
+    const uint32_t logN = 12;
+    size_t kl = dpf_key_len(logN);
+    uint8_t* k = calloc(kl, 1);
+    uint8_t* out = malloc(dpf_evalfull_len(logN));
+    uint64_t x = 5;
+    uint8_t b;
+    void* h = (void*)1;
+    CHECK(dpf_gpu_init(0) == DPF_ERR_NODEV, "init without a GPU");
+    CHECK(strlen(dpf_last_error()) > 0, "no error message");
+    int ord = 0;
+    CHECK(dpf_gpu_init_devices(&ord, 1) == DPF_ERR_NODEV, "init_devices without a GPU");
+    CHECK(dpf_gpu_init_devices(NULL, 0) == DPF_ERR_PARAM, "empty device list");
+    CHECK(dpf_evalfull(k, kl, logN, out) == DPF_ERR_NODEV, "evalfull");
+    CHECK(dpf_evalfull_batch(k, kl, 1, logN, out, 0) == DPF_ERR_NODEV, "evalfull_batch");
+    CHECK(dpf_eval(k, kl, x, logN, &b) == DPF_ERR_NODEV, "eval");
+    CHECK(dpf_eval_batch(k, kl, 1, &x, 1, logN, &b, 0) == DPF_ERR_NODEV, "eval_batch");
+    CHECK(dpf_evalfull_split(k, kl, logN, out, 1) == DPF_ERR_NODEV, "split");
+    CHECK(dpf_pir_db_create(out, 4, logN, 1, &h) == DPF_ERR_NODEV && h == NULL, "pir create");
+    CHECK(dpf_evalfull(k, 16 + 18 * 5, logN, out) == DPF_ERR_KEYLEN, "short key");
+    CHECK(dpf_evalfull(k, kl, 64, out) == DPF_ERR_PARAM, "logN 64");
+    CHECK(dpf_pir_answer(NULL, k, kl, 1, out) == DPF_ERR_PARAM, "null handle");
+    dpf_pir_db_free(NULL);
+    dpf_gpu_shutdown();
+    dpf_gpu_shutdown();
+    CHECK(dpf_gpu_count() == 0, "count after shutdown");
+    CHECK(dpf_evalfull_batch(k, kl, 0, logN, out, 0) == DPF_OK, "empty batch is a no-op");
+    free(k);
+    free(out);
+}
+
+int main(int argc, char** argv) {
+    CHECK(dpf_key_len(20) == 267 && dpf_evalfull_len(20) == 131072 && dpf_evalfull_len(3) == 16, "sizes");
+    gen_checks();
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0)
+        gpu_checks();
+    else
+        nodev_checks();
+    printf("host_sanity ok (%s)\n", argc > 1 ? argv[1] : "nodev");
+    return 0;
+}

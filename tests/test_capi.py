@@ -118,3 +118,54 @@ def test_c_program_runs_on_gpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all checks passed" in r.stdout
+
+
+def _asan_driver(tmp_path, build_lib: bool):
+    """tests/c/host_sanity.c linked against the host-ASan/UBSan build of the
+    library (`make -C dpf-go_amd asan`; sanitizers on host code only)."""
+    import glob
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "dpf-go_amd")
+    libdir = os.path.join(pkg, "lib", "asan")
+    if build_lib:
+        subprocess.run(["make", "-s", "-j4", "-C", pkg, "asan"], check=True, capture_output=True, text=True)
+    if not os.path.exists(os.path.join(libdir, "libdpf_hip.so")):
+        pytest.skip("ASan library not built (make -C dpf-go_amd asan)")
+    clang = "/opt/rocm/lib/llvm/bin/clang"
+    rt = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")
+    if not os.path.exists(clang) or not rt:
+        pytest.skip("no clang ASan runtime")
+    exe = str(tmp_path / "host_sanity")
+    subprocess.run([clang, "-std=c99", "-O1", "-g", "-Wall", "-Werror", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-shared-libasan", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "c", "host_sanity.c"), "-o", exe, "-L", libdir, "-ldpf_hip",
+                    "-Wl,-rpath," + libdir, "-lpthread"], check=True, capture_output=True, text=True)
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = os.path.dirname(rt[0]) + ":" + env.get("LD_LIBRARY_PATH", "")
+    return exe, env
+
+
+def test_host_sanitizers(tmp_path):
+    """ASan (with leak detection) + UBSan over Gen, argument validation,
+    no-device error paths and open/shutdown cycles of the host library."""
+    import subprocess
+    exe, env = _asan_driver(tmp_path, build_lib=True)
+    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "host_sanity ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_host_sanitizers_with_gpu(tmp_path):
+    """The same driver on the GPU box: concurrent host-buffer EvalFull/Eval
+    from 4 threads racing shutdown/re-open, a PIR handle used and freed after
+    shutdown, and a 2 MiB+ CopyPool copy, all under host ASan + UBSan (leak
+    checking off: the HIP runtime keeps process-lifetime allocations)."""
+    import subprocess
+    exe, env = _asan_driver(tmp_path, build_lib=False)
+    env["ASAN_OPTIONS"] = "detect_leaks=0:protect_shadow_gap=0"
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "host_sanity ok (gpu)" in r.stdout

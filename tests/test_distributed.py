@@ -85,3 +85,22 @@ def test_partition_helpers():
     assert [shard.key_range(10, 3, r) for r in range(3)] == [(0, 3), (3, 6), (6, 10)]
     a = np.arange(64, dtype=np.uint8).reshape(2, 32)
     assert np.array_equal(shard.xor_fold(a), a[0] ^ a[1])
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`python bench.py --gpus 2` outside a launcher starts 2 ranks itself
+    (torch.distributed.run as a child) and rank 0 reports n_gpus == 2; the
+    dry run goes through the same launch, barrier and max-over-ranks path
+    as a real run without touching a device."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--steps", "3", "--warmup", "1"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"] and d["local_ranks"] == "2"

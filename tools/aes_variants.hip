@@ -16,7 +16,7 @@
 #include <stdio.h>
 
 #include "../dpf-go_amd/csrc/aes_ttable.hpp"
-#include "../dpf-go_amd/csrc/aes_bitsliced.inc"
+#include "aes_bitsliced.inc"
 
 using namespace dpfk;
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generates dpf-go_amd/csrc/aes_bitsliced.inc: a fully unrolled bitsliced
+"""Generates tools/aes_bitsliced.inc: a fully unrolled bitsliced
 AES-128 encryption for 32 blocks per lane (one u32 per state bit) under the
 fixed PRG keys of dpf/dpf.go:23-24.  Used by tools/aes_variants.hip to
 compare the bitsliced back end with the LDS T-table one on MI355X.
@@ -248,7 +248,7 @@ def main():
     nl = emit("L", KEY_L, out)
     out.append("")
     nr = emit("R", KEY_R, out)
-    dst = os.path.join(ROOT, "dpf-go_amd", "csrc", "aes_bitsliced.inc")
+    dst = os.path.join(HERE, "aes_bitsliced.inc")
     with open(dst, "w") as f:
         f.write("\n".join(out) + "\n")
     print(f"wrote {dst}: {nl} / {nr} bitop3 per 32-block encryption "
