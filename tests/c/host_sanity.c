@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "dpf_hip.h"
 
@@ -231,5 +232,11 @@ int main(int argc, char** argv) {
     else
         nodev_checks();
     printf("host_sanity ok (%s)\n", argc > 1 ? argv[1] : "nodev");
+    fflush(stdout);
+    /* With a GPU, leave without running the HIP runtime's own static
+     * destructors: under host ASan they trip the sanitizer's device-allocator
+     * check (libhsa-runtime64 freeing after ASan's device runtime unloaded),
+     * which is outside this library.  Every check above has already run. */
+    if (argc > 1) _exit(0);
     return 0;
 }
