@@ -256,6 +256,9 @@ class Ctx:
 
 
 def wl_evalfull(c: Ctx) -> dict:
+    """configs[1].  The headline uses the library's AES back end (--aes, or
+    the default); the other back end is timed the same way right after and
+    reported under "aes_variants" (configs[1]: bitsliced vs LDS T-table)."""
     a, dpf, torch = c.args, c.dpf, c.torch
     from dpf import synth
     logN, nk = a.logN, a.nkeys
@@ -274,24 +277,44 @@ def wl_evalfull(c: Ctx) -> dict:
         if ev:
             ev[1].record(c.stream)
 
+    names = {dpf.AES_TTABLE: "lds-ttable", dpf.AES_BITSLICED: "bitsliced"}
+    if a.aes:
+        dpf.set_aes_impl(a.aes)
+    main_impl = dpf.get_aes_impl()
     t_wall, k_ms = c.timed(step, a.steps, a.warmup)
+    sec = t_wall / a.steps
+    aes = nk * aes_full(logN)
+    variants = {names[main_impl]: {"ms_per_step": sec * 1e3, "kernel_ms": k_ms,
+                                   "aes_blocks_per_s": aes / (k_ms * 1e-3),
+                                   "points_per_s": nk * (1 << logN) / sec}}
     if a.check and c.rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         idx = np.unique(np.linspace(0, nk - 1, 8).astype(int))
         got = d_out.view(nk, olen)[torch.from_numpy(idx).to(c.dev)].cpu().numpy()
         assert np.array_equal(got, oracle.evalfull_batch(ka[idx], logN, nthreads=8)), "output differs from oracle"
-    sec = t_wall / a.steps
-    aes = nk * aes_full(logN)
+    if not a.no_variants:
+        other = dpf.AES_BITSLICED if main_impl == dpf.AES_TTABLE else dpf.AES_TTABLE
+        ref = d_out.view(nk, olen)[:64].clone()
+        dpf.set_aes_impl(other)
+        t2, k2 = c.timed(step, max(5, a.steps // 2), 3)
+        dpf.set_aes_impl(main_impl)
+        variants[names[other]] = {"ms_per_step": t2 / max(5, a.steps // 2) * 1e3, "kernel_ms": k2,
+                                  "aes_blocks_per_s": aes / (k2 * 1e-3),
+                                  "points_per_s": nk * (1 << logN) / (t2 / max(5, a.steps // 2)),
+                                  "bit_identical_first_64_keys": bool(torch.equal(ref, d_out.view(nk, olen)[:64]))}
     line = c.line(metric=METRIC, value=nk * (1 << logN) * c.world / sec, unit="points/s",
                   ms_per_step=sec * 1e3, scaling="weak",
                   data="synthetic (SplitMix64 seed 0x5EEDD9F0 keys via host Gen)",
                   config={"workload": f"batched EvalFull, {nk} keys x logN={logN} per GPU (BASELINE configs[1])",
-                          "keys_per_gpu": nk, "logN": logN, "aes": "lds-ttable",
+                          "keys_per_gpu": nk, "logN": logN, "aes": names[main_impl],
                           "parallelism": f"key-shard x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), f"k_evalfull<{min(stop_of(logN), 7)}, true, false>", k_ms,
-                                    nk * olen + nk * (stop_of(logN) + 2) * 32)
+    kern = (f"k_evalfull<{min(stop_of(logN), 7)}, true, false>" if main_impl == dpf.AES_TTABLE
+            else "k_evalfull<NODES>+k_evalfull_bs<true>")
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), kern, k_ms, nk * olen + nk * (stop_of(logN) + 2) * 32,
+                                    aes_impl=names[main_impl])
+    line["aes_variants"] = variants
     return line
 
 
@@ -489,6 +512,9 @@ def main() -> None:
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="split/pir on 1 GPU: time rank 0's share of a W-way split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--aes", choices=["ttable", "bitsliced"], default=None,
+                    help="tree-kernel AES back end for the headline (default: the library's)")
+    ap.add_argument("--no-variants", action="store_true", help="skip timing the other AES back end")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--check", action="store_true", help="verify a sample of outputs against the oracle")
     ap.add_argument("--dry-run", action="store_true",

@@ -1,0 +1,286 @@
+// bs_kernels.hip — EvalFull with the byte-sliced (table-free) AES back end.
+//
+// Reference: evalFullRecursive / EvalFull (dpf/dpf.go:213-262) over prg
+// (dpf.go:59-69) and aes128MMO (dpf/aes_amd64.s:51-82).  Same outputs as the
+// T-table tree kernel (dpf_kernels.hip), bit for bit.
+//
+// Work split (one launch of each):
+//   1. k_evalfull<NODES> (T-table, dpf_kernels.hip) writes the frontier: the
+//      2^f nodes of every key at level f = stop - kBsD (seed + t byte);
+//   2. k_evalfull_bs: a lane takes 8 consecutive frontier nodes as one
+//      byte-sliced set (aes_bytesliced.hpp) and expands them kBsD levels
+//      depth-first.  An expansion is two AES-MMO sets (all 8 nodes under the
+//      left key, then the right key); the 16 children are repacked into the
+//      next two sets of 8 consecutive nodes with one shift + one v_bitop3 per
+//      word (the block order inside a set follows a fixed 3-cycle pattern,
+//      sigma below), so the leaf sets are 8 consecutive leaves = one 128-byte
+//      line per lane, written with 8 back-to-back 16-byte stores.
+// All lanes of a wave run the same DFS (uniform control flow); with >= 64
+// lanes per key (logN >= 20) the wave is one key and the correction words
+// come through scalar loads.  One AES body serves every step (a loop over
+// steps), so the code stays ~1 AES round of instructions.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aes_bytesliced.hpp"
+#include "bs_kernels.hpp"
+#include "dpf_kernels.hpp"
+
+namespace dpfk {
+
+using bs::aes_mmo8;
+using bs::transpose32;
+
+// Byte-sliced correction words: per key, `stop` level records of 36 words
+// (32 sCW planes, then XL, YL, XR, YR) and the final CW (32 planes).
+// Plane word (8*row + plane), byte c = 0xFF iff bit `plane` of CW byte
+// (c, row) is set.  t classes (tCW byte v): X = v == 1, Y = v > 1 (as masks),
+// so that a child's "t != 0" is  tp ? ((b ^ X) | Y) : b  for its raw bit b
+// (dpf.go:185-193,230-238: t bytes XOR as bytes, tested != 0).
+constexpr uint32_t kBsRec = 36;
+
+__host__ __device__ uint64_t bs_key_words(uint32_t stop) { return (uint64_t)stop * kBsRec + 32; }
+
+__device__ __forceinline__ uint32_t planes_word(const uint8_t* p, uint32_t row, uint32_t plane) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        if ((p[4 * c + row] >> plane) & 1u) v |= 0xFFu << (8 * c);
+    return v;
+}
+
+// One thread per (key, record): record r < stop = level r, r == stop = final CW.
+__global__ void k_unpack_bs(const uint8_t* __restrict__ keys, uint64_t key_len, uint64_t nkeys, uint32_t stop,
+                            uint32_t* __restrict__ ekb) {
+    const uint64_t recs = (uint64_t)stop + 1;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nkeys * recs) return;
+    const uint64_t k = i / recs, r = i % recs;
+    const uint8_t* kp = keys + k * key_len;
+    uint32_t* o = ekb + k * bs_key_words(stop) + r * kBsRec;
+    const uint8_t* p = r < stop ? kp + 17 + 18 * r : kp + key_len - 16;   // dpf.go:231-233 / :206,219
+    for (uint32_t w = 0; w < 32; ++w) o[w] = planes_word(p, w >> 3, w & 7);
+    if (r < stop) {
+        const uint8_t tl = p[16], tr = p[17];
+        o[32] = tl == 1 ? ~0u : 0u;
+        o[33] = tl > 1 ? ~0u : 0u;
+        o[34] = tr == 1 ? ~0u : 0u;
+        o[35] = tr > 1 ? ~0u : 0u;
+    }
+}
+
+// Child set after aes_mmo8 (o = MMO(x)): split the control bits off (byte 0
+// of row 0 / plane 0), clear them, apply the parent's correction (dpf.go:
+// 61-68,230-238).  tp: parent "t != 0" mask (bit i of every byte = block i).
+__device__ __forceinline__ uint32_t child_fix(uint32_t (&o)[32], uint32_t tp, const uint32_t* __restrict__ cw,
+                                              uint32_t side) {
+    const uint32_t b = __builtin_amdgcn_perm(o[0], o[0], 0u);   // raw t bits, broadcast to 4 bytes
+    o[0] &= 0xFFFFFF00u;
+#pragma unroll
+    for (int w = 0; w < 32; ++w) o[w] = __builtin_amdgcn_bitop3_b32(o[w], tp, cw[w], 0x78);   // o ^ (tp & cw)
+    const uint32_t X = cw[32 + 2 * side], Y = cw[33 + 2 * side];
+    return (tp & ((b ^ X) | Y)) | (~tp & b);
+}
+
+// Repack children of 8 consecutive nodes: L/R sets (same block order) ->
+// A = first 8 children, B = last 8.  Shift s and mask m by depth (see sigma).
+__device__ __forceinline__ uint32_t rp_a(uint32_t l, uint32_t r, uint32_t s, uint32_t m) {
+    return __builtin_amdgcn_bitop3_b32(l, r << s, m, 0xe4);   // m ? l : r << s
+}
+__device__ __forceinline__ uint32_t rp_b(uint32_t l, uint32_t r, uint32_t s, uint32_t m) {
+    return __builtin_amdgcn_bitop3_b32(l >> s, r, m, 0xe4);   // m ? l >> s : r
+}
+
+#define DPF_BS_COPY(DST, SRC) _Pragma("unroll") for (int w_ = 0; w_ < 32; ++w_) DST[w_] = SRC[w_];
+#define DPF_BS_PUSH_LDS(SLOT, SRC) \
+    _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_) \
+        lds[SLOT][q_][lane] = make_uint4(SRC[4 * q_], SRC[4 * q_ + 1], SRC[4 * q_ + 2], SRC[4 * q_ + 3]);
+#define DPF_BS_POP_LDS(SLOT, DST) \
+    _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_) { \
+        const uint4 v_ = lds[SLOT][q_][lane]; \
+        DST[4 * q_] = v_.x; DST[4 * q_ + 1] = v_.y; DST[4 * q_ + 2] = v_.z; DST[4 * q_ + 3] = v_.w; \
+    }
+
+constexpr int kBsBlock = 256;
+
+// Thread u: key u >> (flog - 3), frontier nodes 8*(u mod 2^(flog-3)) .. +7
+// of that key (level lvl0; 2^flog frontier nodes per key).  Output: 2^kBsD
+// leaves of 16 B below each node, at out + key * out_stride.
+template <bool UNIFORM>
+__global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __restrict__ fseed,
+                                                        const uint8_t* __restrict__ ft, uint32_t flog,
+                                                        const uint32_t* __restrict__ ekb, uint32_t stop,
+                                                        uint32_t lvl0, uint64_t nthreads, uint8_t* __restrict__ out,
+                                                        uint64_t out_stride) {
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nthreads) return;
+    const uint32_t glog = flog - 3;
+    uint64_t key = u >> glog;
+    if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
+    const uint64_t g = u & ((1ull << glog) - 1);
+    const uint64_t node0 = (key << flog) + 8 * g;
+    const uint32_t* ek = ekb + key * bs_key_words(stop);
+    const uint32_t* fcw = ek + (uint64_t)stop * kBsRec;
+    uint8_t* obase = out + key * out_stride + ((g * 8) << kBsD) * 16;
+
+    uint32_t X[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {                 // M[8c + i] = word c of block i
+        const uint4 v = fseed[node0 + i];
+        X[i] = v.x; X[8 + i] = v.y; X[16 + i] = v.z; X[24 + i] = v.w;
+    }
+    transpose32(X);
+    uint32_t tX = 0;
+    {
+        const uint2 tw = *reinterpret_cast<const uint2*>(ft + node0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t byte = ((i < 4 ? tw.x : tw.y) >> (8 * (i & 3))) & 0xFFu;
+            tX |= (byte != 0 ? 1u : 0u) << i;
+        }
+        tX *= 0x01010101u;
+    }
+
+    // DFS stack of pending right sets: depths 2, 3 in VGPRs, depths 0, 1 (the
+    // least used: pushed once / twice per lane) in this wave's LDS rows --
+    // the register budget at 2 waves/SIMD (256 per lane) holds the AES
+    // state, its feed-forward input, the left child set and two slots only.
+    __shared__ uint4 s_stack[kBsBlock / 64][2][8][64];
+    uint4 (*lds)[8][64] = s_stack[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t L[32], S2[32], S3[32];
+    uint32_t tL = 0, tS0 = 0, tS1 = 0, tS2 = 0, tS3 = 0;
+    uint32_t d = 0, path = 0, phase = 0;   // phase 0/1: left/right AES of an expansion, 2: leaf
+    for (;;) {
+        uint32_t O[32];
+        aes_mmo8(X, O, phase == 1 ? 1u : 0u);
+        if (phase == 0) {
+            tL = child_fix(O, tX, ek + (uint64_t)(lvl0 + d) * kBsRec, 0);
+            DPF_BS_COPY(L, O)
+            phase = 1;
+            continue;
+        }
+        if (phase == 1) {
+            const uint32_t tR = child_fix(O, tX, ek + (uint64_t)(lvl0 + d) * kBsRec, 1);
+            // shift / mask cycle by depth: 4 / 0x0F, 2 / 0x33, 1 / 0x55
+            const uint32_t dm = d % 3;
+            const uint32_t s = dm == 0 ? 4u : dm == 1 ? 2u : 1u;
+            const uint32_t m = dm == 0 ? 0x0F0F0F0Fu : dm == 1 ? 0x33333333u : 0x55555555u;
+            uint32_t B[32];
+#pragma unroll
+            for (int w = 0; w < 32; ++w) {
+                X[w] = rp_a(L[w], O[w], s, m);
+                B[w] = rp_b(L[w], O[w], s, m);
+            }
+            const uint32_t tB = rp_b(tL, tR, s, m);
+            tX = rp_a(tL, tR, s, m);
+            switch (d) {                            // push B (static register slots / LDS rows)
+                case 0: DPF_BS_PUSH_LDS(0, B) tS0 = tB; break;
+                case 1: DPF_BS_PUSH_LDS(1, B) tS1 = tB; break;
+                case 2: DPF_BS_COPY(S2, B) tS2 = tB; break;
+                default: DPF_BS_COPY(S3, B) tS3 = tB; break;
+            }
+            ++d;
+            path <<= 1;
+            phase = d < kBsD ? 0 : 2;
+            continue;
+        }
+        // Leaf set: 8 consecutive leaves 8*path + sigma(i) (dpf.go:214-224).
+#pragma unroll
+        for (int w = 0; w < 32; ++w) O[w] = __builtin_amdgcn_bitop3_b32(O[w], tX, fcw[w], 0x78);
+        transpose32(O);
+        {
+            uint8_t* p = obase + (uint64_t)path * 128;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                *reinterpret_cast<uint4*>(p + 16 * kBsSigmaLeaf[i]) = make_uint4(O[i], O[8 + i], O[16 + i], O[24 + i]);
+        }
+        while (d > 0 && (path & 1u)) {          // climb over finished right branches
+            path >>= 1;
+            --d;
+        }
+        if (d == 0) break;
+        switch (d - 1) {                        // pop the pending right set of depth d-1
+            case 0: DPF_BS_POP_LDS(0, X) tX = tS0; break;
+            case 1: DPF_BS_POP_LDS(1, X) tX = tS1; break;
+            case 2: DPF_BS_COPY(X, S2) tX = tS2; break;
+            default: DPF_BS_COPY(X, S3) tX = tS3; break;
+        }
+        path |= 1u;
+        phase = d < kBsD ? 0 : 2;
+    }
+}
+
+hipError_t launch_unpack_bs(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ekb,
+                            hipStream_t st) {
+    const uint64_t n = nkeys * ((uint64_t)stop + 1);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpack_bs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, keys, key_len, nkeys, stop,
+                       ekb);
+    return hipGetLastError();
+}
+
+bool bs_applicable(uint32_t stop, uint32_t prefix_bits) {
+    return stop >= prefix_bits + kBsD + 3;   // >= 8 frontier nodes per key below the prefix
+}
+
+uint64_t bs_frontier_bytes(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits) {
+    if (!bs_applicable(stop, prefix_bits)) return 0;
+    const uint64_t n = nkeys << (stop - kBsD - prefix_bits);
+    return (n * 16 + n + 255) & ~255ull;
+}
+
+hipError_t launch_evalfull_bs(const uint32_t* ek, const uint32_t* ekb, uint64_t nkeys, uint32_t stop,
+                              uint32_t prefix_bits, uint64_t prefix, uint8_t* out, uint64_t out_stride, void* frontier,
+                              hipStream_t st) {
+    if (nkeys == 0) return hipSuccess;
+    if (!bs_applicable(stop, prefix_bits)) return hipErrorInvalidValue;
+    const uint32_t f = stop - kBsD;                 // frontier level
+    const uint32_t flog = f - prefix_bits;          // frontier nodes per key below the prefix
+    uint8_t* fs = static_cast<uint8_t*>(frontier);
+    uint8_t* fts = fs + (nkeys << flog) * 16;
+    hipError_t e = launch_nodes(ek, nkeys, stop, f, prefix_bits, prefix, fs, fts, 1ull << flog, st);
+    if (e != hipSuccess) return e;
+    const uint64_t threads = nkeys << (flog - 3);
+    const dim3 grid((uint32_t)((threads + kBsBlock - 1) / kBsBlock));
+    if (flog - 3 >= 6)
+        hipLaunchKernelGGL(k_evalfull_bs<true>, grid, dim3(kBsBlock), 0, st, reinterpret_cast<const uint4*>(fs), fts, flog,
+                           ekb, stop, f, threads, out, out_stride);
+    else
+        hipLaunchKernelGGL(k_evalfull_bs<false>, grid, dim3(kBsBlock), 0, st, reinterpret_cast<const uint4*>(fs), fts,
+                           flog, ekb, stop, f, threads, out, out_stride);
+    return hipGetLastError();
+}
+
+// 8 independent blocks per lane through the byte-sliced MMO (AES
+// microbenchmark / self-test entry): in/out [n][16] bytes, n % 8 == 0.
+__global__ __launch_bounds__(256) void k_mmo_bs(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t nsets,
+                                                uint32_t key, uint32_t reps) {
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nsets) return;
+    uint32_t X[32], O[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 v = in[u * 8 + i];
+        X[i] = v.x; X[8 + i] = v.y; X[16 + i] = v.z; X[24 + i] = v.w;
+    }
+    transpose32(X);
+    for (uint32_t r = 0; r < reps; ++r) {
+        aes_mmo8(X, O, key);
+        DPF_BS_COPY(X, O)
+    }
+    transpose32(X);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[u * 8 + i] = make_uint4(X[i], X[8 + i], X[16 + i], X[24 + i]);
+}
+
+hipError_t launch_mmo_bs(const uint8_t* in, uint8_t* out, uint64_t nblocks, uint32_t key, uint32_t reps,
+                         hipStream_t st) {
+    const uint64_t sets = nblocks / 8;
+    if (sets == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mmo_bs, dim3((uint32_t)((sets + 255) / 256)), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), sets, key, reps);
+    return hipGetLastError();
+}
+
+}  // namespace dpfk

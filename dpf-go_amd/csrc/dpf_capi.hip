@@ -21,6 +21,7 @@
 
 #include "../../include/dpf_hip.h"
 #include "dpf_internal.hpp"
+#include "bs_kernels.hpp"
 #include "dpf_kernels.hpp"
 #include "pir_kernels.hpp"
 
@@ -284,6 +285,56 @@ int check_key(size_t klen, uint32_t logN) {
     return DPF_OK;
 }
 
+// ---- AES back end of the tree kernels (configs[1]: bitsliced vs T-table) --
+// DPF_AES_IMPL=bitsliced|ttable sets the default; dpf_set_aes_impl switches
+// at run time.  Both give bit-identical outputs.
+std::atomic<int> g_aes_impl{[] {
+    const char* e = getenv("DPF_AES_IMPL");
+    return e && (e[0] == 'b' || e[0] == 'B') ? DPF_AES_BITSLICED : DPF_AES_TTABLE;
+}()};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Tree workspace for nk expanded keys: [T-table records | byte-sliced CW
+// words | byte-sliced frontier for up to `chunk` keys per launch].
+size_t tree_ws_bytes(size_t nk, uint32_t stop, uint32_t prefix_bits, size_t chunk) {
+    return align256(nk * dpfk::ek_words(stop) * 4) + align256(nk * dpfk::bs_key_words(stop) * 4) +
+           dpfk::bs_frontier_bytes(chunk, stop, prefix_bits);
+}
+
+struct TreeWs {
+    uint32_t* ek;
+    uint32_t* ekb;
+    void* frontier;
+};
+
+TreeWs tree_ws(void* work, size_t nk, uint32_t stop) {
+    uint8_t* p = static_cast<uint8_t*>(work);
+    TreeWs w;
+    w.ek = reinterpret_cast<uint32_t*>(p);
+    p += align256(nk * dpfk::ek_words(stop) * 4);
+    w.ekb = reinterpret_cast<uint32_t*>(p);
+    p += align256(nk * dpfk::bs_key_words(stop) * 4);
+    w.frontier = p;
+    return w;
+}
+
+// Key records for both back ends (the byte-sliced words are 3% of a tree launch at configs[1]).
+hipError_t expand_keys(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t stop, const TreeWs& w, hipStream_t st) {
+    hipError_t e = dpfk::launch_unpack(d_keys, klen, nk, stop, w.ek, st);
+    if (e != hipSuccess) return e;
+    return dpfk::launch_unpack_bs(d_keys, klen, nk, stop, w.ekb, st);
+}
+
+// Leaves of subtree (prefix_bits, prefix) of keys [k0, k0 + n) through the selected back end.
+hipError_t run_tree(const TreeWs& w, size_t k0, size_t n, uint32_t stop, uint32_t prefix_bits, uint64_t prefix,
+                    uint8_t* out, uint64_t stride, hipStream_t st) {
+    if (g_aes_impl.load(std::memory_order_relaxed) == DPF_AES_BITSLICED && dpfk::bs_applicable(stop, prefix_bits))
+        return dpfk::launch_evalfull_bs(w.ek + k0 * dpfk::ek_words(stop), w.ekb + k0 * dpfk::bs_key_words(stop), n, stop,
+                                        prefix_bits, prefix, out, stride, w.frontier, st);
+    return dpfk::launch_evalfull(w.ek + k0 * dpfk::ek_words(stop), n, stop, prefix_bits, prefix, out, stride, st);
+}
+
 // Evaluate subtree (prefix_bits, prefix) of nk keys already resident at
 // d_keys into d_out (2^(stop-prefix_bits) leaves per key), on stream st.
 int enqueue_full(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t logN, uint32_t prefix_bits,
@@ -348,18 +399,17 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
     DeviceGuard g(d.id);
     const uint32_t stop = stop_of(logN);
     const size_t olen = full_len(logN);
-    const size_t ekw = dpfk::ek_words(stop);
+    const size_t per = olen <= kStageBytes ? kStageBytes / olen : 1;   // keys per chunk
     HIP_TRY(hipError_t(d.keys.ensure(nk * klen)));
-    HIP_TRY(hipError_t(d.work.ensure(nk * ekw * 4)));
+    HIP_TRY(hipError_t(d.work.ensure(tree_ws_bytes(nk, stop, 0, std::min(per, nk)))));
     HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
-    HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, nk, stop, (uint32_t*)d.work.p, d.st));
-    const uint32_t* ek = (const uint32_t*)d.work.p;
+    const TreeWs w = tree_ws(d.work.p, nk, stop);
+    HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, nk, stop, w, d.st));
     if (olen <= kStageBytes) {
-        const size_t per = kStageBytes / olen;            // keys per chunk
         const size_t nch = (nk + per - 1) / per;
         return pipeline_d2h(d, nch, std::min(per, nk) * olen, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
             const size_t k0 = i * per, n = std::min(per, nk - k0);
-            HIP_TRY(dpfk::launch_evalfull(ek + k0 * ekw, n, stop, 0, 0, dbuf, olen, d.st));
+            HIP_TRY(run_tree(w, k0, n, stop, 0, 0, dbuf, olen, d.st));
             bytes = n * olen;
             off = k0 * olen;
             return DPF_OK;
@@ -370,7 +420,7 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
     const size_t slab = olen >> pb, per_key = (size_t)1 << pb;
     return pipeline_d2h(d, nk * per_key, slab, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
         const size_t k = i / per_key, p = i % per_key;
-        HIP_TRY(dpfk::launch_evalfull(ek + k * ekw, 1, stop, pb, p, dbuf, slab, d.st));
+        HIP_TRY(run_tree(w, k, 1, stop, pb, p, dbuf, slab, d.st));
         bytes = slab;
         off = k * olen + p * slab;
         return DPF_OK;
@@ -486,7 +536,26 @@ const char* dpf_last_error(void) { return t_err.c_str(); }
 size_t dpf_key_len(uint32_t logN) { return key_len(logN); }
 size_t dpf_evalfull_len(uint32_t logN) { return full_len(logN); }
 size_t dpf_workspace_size(size_t nkeys, uint32_t logN) {
-    return std::max<size_t>(16, nkeys * dpfk::ek_words(stop_of(logN)) * 4);
+    return std::max<size_t>(16, tree_ws_bytes(nkeys, stop_of(logN), 0, nkeys));
+}
+
+int dpf_set_aes_impl(int impl) {
+    if (impl != DPF_AES_TTABLE && impl != DPF_AES_BITSLICED) return fail(DPF_ERR_PARAM, "dpf: unknown AES back end");
+    return g_aes_impl.exchange(impl);
+}
+
+int dpf_get_aes_impl(void) { return g_aes_impl.load(); }
+
+int dpf_aes_mmo_dev(int device, int impl, int right, const uint8_t* d_in, uint8_t* d_out, size_t nblocks,
+                    uint32_t reps, void* stream) {
+    if (impl != DPF_AES_TTABLE && impl != DPF_AES_BITSLICED) return fail(DPF_ERR_PARAM, "dpf: unknown AES back end");
+    if (nblocks % 8) return fail(DPF_ERR_PARAM, "dpf: nblocks must be a multiple of 8");
+    DeviceGuard g(device);
+    if (impl == DPF_AES_BITSLICED)
+        HIP_TRY(dpfk::launch_mmo_bs(d_in, d_out, nblocks, right ? 1u : 0u, reps, (hipStream_t)stream));
+    else
+        HIP_TRY(dpfk::launch_mmo_tt(d_in, d_out, nblocks, right ? 1u : 0u, reps, (hipStream_t)stream));
+    return DPF_OK;
 }
 
 int dpf_gpu_init(int ngpus) { return open_devices(ngpus); }
@@ -587,16 +656,16 @@ int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* 
         std::lock_guard<std::mutex> lk(d.mu);
         DeviceGuard gd(d.id);
         HIP_TRY(hipError_t(d.keys.ensure(klen)));
-        HIP_TRY(hipError_t(d.work.ensure(dpfk::ek_words(stop) * 4)));
+        HIP_TRY(hipError_t(d.work.ensure(tree_ws_bytes(1, stop, pb, 1))));
         HIP_TRY(hipMemcpyAsync(d.keys.p, key, klen, hipMemcpyHostToDevice, d.st));
-        HIP_TRY(dpfk::launch_unpack((const uint8_t*)d.keys.p, klen, 1, stop, (uint32_t*)d.work.p, d.st));
+        const TreeWs w = tree_ws(d.work.p, 1, stop);
+        HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, 1, stop, w, d.st));
         // This device's subtree (pb, lo), streamed out in sub-slabs (pb + extra, lo * 2^extra + j).
         uint32_t extra = 0;
         while ((slab >> extra) > kStageBytes && pb + extra < stop) ++extra;
         const size_t sub = slab >> extra;
         return pipeline_d2h(d, (size_t)1 << extra, sub, [&](size_t j, uint8_t* dbuf, size_t& bytes, size_t& off) {
-            HIP_TRY(dpfk::launch_evalfull((const uint32_t*)d.work.p, 1, stop, pb + extra, ((uint64_t)lo << extra) + j,
-                                          dbuf, sub, d.st));
+            HIP_TRY(run_tree(w, 0, 1, stop, pb + extra, ((uint64_t)lo << extra) + j, dbuf, sub, d.st));
             bytes = sub;
             off = lo * slab + j * sub;
             return DPF_OK;
@@ -612,8 +681,11 @@ int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t klen, siz
         return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
     if (nkeys == 0) return DPF_OK;
     DeviceGuard g(device);
-    return enqueue_full(d_keys, klen, nkeys, logN, prefix_bits, prefix, d_out, (uint32_t*)d_work,
-                        (hipStream_t)stream);
+    const TreeWs w = tree_ws(d_work, nkeys, stop);
+    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, (hipStream_t)stream));
+    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, d_out, (uint64_t)16 << (stop - prefix_bits),
+                     (hipStream_t)stream));
+    return DPF_OK;
 }
 
 int dpf_evalfull_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN,
@@ -645,7 +717,7 @@ int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t klen, size_t n
                         void* stream) {
     if (int rc = check_key(klen, logN)) return rc;
     DeviceGuard g(device);
-    HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop_of(logN), (uint32_t*)d_work, (hipStream_t)stream));
+    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop_of(logN), tree_ws(d_work, nkeys, stop_of(logN)), (hipStream_t)stream));
     return DPF_OK;
 }
 
@@ -657,8 +729,8 @@ int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint
     if (nkeys == 0) return DPF_OK;
     DeviceGuard g(device);
     const uint64_t stride = (uint64_t)16 << (stop - prefix_bits);
-    HIP_TRY(dpfk::launch_evalfull((const uint32_t*)d_work, nkeys, stop, prefix_bits, prefix, d_out, stride,
-                                  (hipStream_t)stream));
+    HIP_TRY(run_tree(tree_ws(const_cast<void*>(d_work), nkeys, stop), 0, nkeys, stop, prefix_bits, prefix, d_out, stride,
+                     (hipStream_t)stream));
     return DPF_OK;
 }
 

@@ -266,7 +266,39 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     out[q] = (uint8_t)((w >> (b & 31)) & 1u);
 }
 
+// aes128MMO microbenchmark / self-test on the T-table back end: two
+// independent blocks per thread (the PRG's own ILP), iterated `reps` times.
+template <bool RIGHT>
+__global__ __launch_bounds__(kBlock, 4) void k_mmo_tt(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                      uint64_t npairs, uint32_t reps) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+    fill_table(s_tab);
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= npairs) return;
+    const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
+    const uint32_t lo = (threadIdx.x & 31u) * 4u;
+    const uint4 va = in[2 * u], vb = in[2 * u + 1];
+    Blk a = {va.x, va.y, va.z, va.w}, b = {vb.x, vb.y, vb.z, vb.w};
+    for (uint32_t r = 0; r < reps; ++r) mmo_pair(tab, lo, KeyFixed<RIGHT>{}, a, a, KeyFixed<RIGHT>{}, b, b);
+    out[2 * u] = make_uint4(a.c0, a.c1, a.c2, a.c3);
+    out[2 * u + 1] = make_uint4(b.c0, b.c1, b.c2, b.c3);
+}
+
 // ------------------------------------------------------------ launchers ---
+
+hipError_t launch_mmo_tt(const uint8_t* in, uint8_t* out, uint64_t nblocks, uint32_t right, uint32_t reps,
+                         hipStream_t st) {
+    const uint64_t pairs = nblocks / 2;
+    if (pairs == 0) return hipSuccess;
+    const dim3 grid((uint32_t)((pairs + kBlock - 1) / kBlock));
+    if (right)
+        hipLaunchKernelGGL(k_mmo_tt<true>, grid, dim3(kBlock), 0, st, reinterpret_cast<const uint4*>(in),
+                           reinterpret_cast<uint4*>(out), pairs, reps);
+    else
+        hipLaunchKernelGGL(k_mmo_tt<false>, grid, dim3(kBlock), 0, st, reinterpret_cast<const uint4*>(in),
+                           reinterpret_cast<uint4*>(out), pairs, reps);
+    return hipGetLastError();
+}
 
 hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ek,
                          hipStream_t st) {
@@ -380,6 +412,11 @@ static hipError_t launch_tree(const uint32_t* ek, uint64_t nkeys, uint32_t stop,
         default: DPF_LAUNCH(7);
     }
 #undef DPF_LAUNCH
+}
+
+hipError_t launch_nodes(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t depth, uint32_t prefix_bits,
+                        uint64_t prefix, uint8_t* seeds, uint8_t* ts, uint64_t stride, hipStream_t st) {
+    return launch_tree<true>(ek, nkeys, stop, depth, prefix_bits, prefix, seeds, ts, stride, st);
 }
 
 hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,

@@ -22,6 +22,10 @@ constexpr uint32_t kMaxFrontierHbm = 16;  // batched Eval, HBM frontier: deepest
 // Expanded-key words per key: (stop + 2) records of 8 u32.
 inline uint64_t ek_words(uint32_t stop) { return ((uint64_t)stop + 2) * 8; }
 
+// aes128MMO iterated `reps` times over nblocks (even) blocks, T-table back end.
+hipError_t launch_mmo_tt(const uint8_t* in, uint8_t* out, uint64_t nblocks, uint32_t right, uint32_t reps,
+                         hipStream_t st);
+
 hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ek,
                          hipStream_t st);
 
@@ -30,6 +34,12 @@ hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, 
 // prefix_bits) leaves of 16 B at out + key * out_stride.
 hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
                            uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st);
+
+// The 2^(depth - prefix_bits) nodes at level `depth` below prefix node
+// (prefix_bits, prefix) of every key: seeds (16 B) at seeds + (key * stride
+// + j) * 16 and t bytes at ts + key * stride + j.
+hipError_t launch_nodes(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t depth, uint32_t prefix_bits,
+                        uint64_t prefix, uint8_t* seeds, uint8_t* ts, uint64_t stride, hipStream_t st);
 
 // Batched Eval.  When a key has enough points to share the top of its tree
 // (2^(L+2) <= pts_per_key), the 2^L nodes at level L of every key are first

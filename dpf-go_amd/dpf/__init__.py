@@ -32,6 +32,8 @@ DPF_ERR_KEYLEN = -2
 DPF_ERR_NODEV = -3
 DPF_ERR_HIP = -4
 DPF_ERR_NOMEM = -5
+AES_TTABLE = 0
+AES_BITSLICED = 1
 
 
 class DPFPanic(RuntimeError):
@@ -74,6 +76,9 @@ SIGNATURES = {
     "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _sz, _vp]),
     "dpf_expand_keys_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp]),
     "dpf_evalfull_expanded_dev": (_int, [_int, _vp, _sz, _u32, _u32, _u64, _vp, _vp]),
+    "dpf_set_aes_impl": (_int, [_int]),
+    "dpf_get_aes_impl": (_int, []),
+    "dpf_aes_mmo_dev": (_int, [_int, _int, _int, _vp, _vp, _sz, _u32, _vp]),
     "dpf_pir_workspace_size": (_sz, [_sz, _u32, _u32]),
     "dpf_pir_answer_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _u64, _vp, _vp, _vp]),
     "dpf_pir_db_create": (_int, [_u8p, _u64, _u32, _int, ctypes.POINTER(_vp)]),
@@ -289,6 +294,27 @@ def evalfull_expanded_dev(d_work, nkeys: int, logN: int, d_out, prefix_bits: int
                           device: int = 0, stream=None) -> None:
     _check(lib().dpf_evalfull_expanded_dev(device, _ptr(d_work), nkeys, logN, prefix_bits, prefix, _ptr(d_out),
                                            _stream_handle(stream)))
+
+
+def set_aes_impl(impl) -> int:
+    """Select the tree kernels' AES back end ("ttable"/"bitsliced" or 0/1); returns the previous one."""
+    if isinstance(impl, str):
+        impl = {"ttable": AES_TTABLE, "lds-ttable": AES_TTABLE, "bitsliced": AES_BITSLICED}[impl]
+    rc = lib().dpf_set_aes_impl(impl)
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+def get_aes_impl() -> int:
+    return int(lib().dpf_get_aes_impl())
+
+
+def aes_mmo_dev(d_in, d_out, nblocks: int, impl: int = AES_TTABLE, right: bool = False, reps: int = 1,
+                device: int = 0, stream=None) -> None:
+    """aes128MMO iterated `reps` times over nblocks HBM blocks (both back ends)."""
+    _check(lib().dpf_aes_mmo_dev(device, impl, 1 if right else 0, _ptr(d_in), _ptr(d_out), nblocks, reps,
+                                 _stream_handle(stream)))
 
 
 # ------------------------------------------------------------------ PIR ---

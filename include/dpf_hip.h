@@ -115,6 +115,22 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t
                        size_t pts_per_key, uint32_t logN, uint8_t* d_out, void* d_work, size_t work_bytes,
                        void* stream);
 
+/* ---- AES back end of the tree kernels (BASELINE configs[1]) ------------
+ * DPF_AES_TTABLE: T-tables staged in LDS (aes_ttable.hpp).
+ * DPF_AES_BITSLICED: table-free byte-sliced AES, 8 blocks per lane in VALU
+ * registers (aes_bytesliced.hpp); used for EvalFull subtrees of >= 2^7 leaf
+ * blocks per key, the T-table elsewhere.  Outputs are bit-identical.
+ * Process-wide; the default comes from env DPF_AES_IMPL=ttable|bitsliced. */
+#define DPF_AES_TTABLE 0
+#define DPF_AES_BITSLICED 1
+int dpf_set_aes_impl(int impl);   /* returns the previous back end */
+int dpf_get_aes_impl(void);
+/* aes128MMO (aes_amd64.s:51-82) of nblocks (multiple of 8) 16-byte blocks,
+ * iterated `reps` times (out = MMO^reps(in)), under the fixed left (right=0)
+ * or right key (dpf.go:23-24): the AES blocks/s microbenchmark + self-test. */
+int dpf_aes_mmo_dev(int device, int impl, int right, const uint8_t* d_in, uint8_t* d_out, size_t nblocks,
+                    uint32_t reps, void* stream);
+
 /* Two-phase form of the above: expand keys once into d_work (the aligned
  * per-level records the kernels read), then evaluate any number of
  * subtrees from the expanded form.  Lets a caller time the tree kernel
