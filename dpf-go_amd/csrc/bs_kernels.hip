@@ -91,6 +91,18 @@ __device__ __forceinline__ uint32_t rp_b(uint32_t l, uint32_t r, uint32_t s, uin
     return __builtin_amdgcn_bitop3_b32(l >> s, r, m, 0xe4);   // m ? l >> s : r
 }
 
+// Leaf conversion of a set (MMO_L output o, leaf t mask tl): ^ (t ? finalCW :
+// 0), back to 8 blocks, 8 consecutive 16-byte stores (one 128-byte line).
+__device__ __forceinline__ void leaf_store(uint32_t (&o)[32], uint32_t tl, const uint32_t* __restrict__ fcw,
+                                           uint8_t* p) {
+#pragma unroll
+    for (int w = 0; w < 32; ++w) o[w] = __builtin_amdgcn_bitop3_b32(o[w], tl, fcw[w], 0x78);
+    transpose32(o);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        *reinterpret_cast<uint4*>(p + 16 * kBsSigmaLeaf[i]) = make_uint4(o[i], o[8 + i], o[16 + i], o[24 + i]);
+}
+
 #define DPF_BS_COPY(DST, SRC) _Pragma("unroll") for (int w_ = 0; w_ < 32; ++w_) DST[w_] = SRC[w_];
 #define DPF_BS_PUSH_LDS(SLOT, SRC) \
     _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_) \
@@ -141,73 +153,72 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
         tX *= 0x01010101u;
     }
 
-    // DFS stack of pending right sets: depths 2, 3 in VGPRs, depths 0, 1 (the
-    // least used: pushed once / twice per lane) in this wave's LDS rows --
-    // the register budget at 2 waves/SIMD (256 per lane) holds the AES
-    // state, its feed-forward input, the left child set and two slots only.
+    // Depth-first over sets.  An iteration expands X (depth d < kBsD, set
+    // index `path` among the 2^d sets of the lane at that depth): left and
+    // right AES-MMO sets, repack into A (first 8 children) and B (last 8).
+    // Above the leaves A is expanded next and B waits in a stack slot; at
+    // the bottom A and B are leaf sets.  Four AES call sites, no per-step
+    // register copies besides the stack.
+    // Stack of pending right sets: depth 2 in VGPRs; depths 0 and 1 (pushed
+    // once / twice per lane) in this wave's LDS rows, which leaves the AES
+    // rounds ~180 VGPRs to schedule in at 2 waves/SIMD.
     __shared__ uint4 s_stack[kBsBlock / 64][2][8][64];
     uint4 (*lds)[8][64] = s_stack[threadIdx.x >> 6];
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t L[32], S2[32], S3[32];
-    uint32_t tL = 0, tS0 = 0, tS1 = 0, tS2 = 0, tS3 = 0;
-    uint32_t d = 0, path = 0, phase = 0;   // phase 0/1: left/right AES of an expansion, 2: leaf
+    uint32_t S2[32];
+    uint32_t tS0 = 0, tS1 = 0, tS2 = 0;
+    uint32_t d = 0, path = 0;
     for (;;) {
-        uint32_t O[32];
-        aes_mmo8(X, O, phase == 1 ? 1u : 0u);
-        if (phase == 0) {
-            tL = child_fix(O, tX, ek + (uint64_t)(lvl0 + d) * kBsRec, 0);
-            DPF_BS_COPY(L, O)
-            phase = 1;
-            continue;
-        }
-        if (phase == 1) {
-            const uint32_t tR = child_fix(O, tX, ek + (uint64_t)(lvl0 + d) * kBsRec, 1);
-            // shift / mask cycle by depth: 4 / 0x0F, 2 / 0x33, 1 / 0x55
-            const uint32_t dm = d % 3;
-            const uint32_t s = dm == 0 ? 4u : dm == 1 ? 2u : 1u;
-            const uint32_t m = dm == 0 ? 0x0F0F0F0Fu : dm == 1 ? 0x33333333u : 0x55555555u;
-            uint32_t B[32];
+        const uint32_t* cw = ek + (uint64_t)(lvl0 + d) * kBsRec;
+        uint32_t L[32], R[32], B[32];
+        aes_mmo8(X, L, 0);
+        const uint32_t tL = child_fix(L, tX, cw, 0);
+        aes_mmo8(X, R, 1);
+        const uint32_t tR = child_fix(R, tX, cw, 1);
+        // shift / mask cycle by depth: 4 / 0x0F, 2 / 0x33, 1 / 0x55
+        const uint32_t dm = d % 3;
+        const uint32_t sh = dm == 0 ? 4u : dm == 1 ? 2u : 1u;
+        const uint32_t m = dm == 0 ? 0x0F0F0F0Fu : dm == 1 ? 0x33333333u : 0x55555555u;
 #pragma unroll
-            for (int w = 0; w < 32; ++w) {
-                X[w] = rp_a(L[w], O[w], s, m);
-                B[w] = rp_b(L[w], O[w], s, m);
-            }
-            const uint32_t tB = rp_b(tL, tR, s, m);
-            tX = rp_a(tL, tR, s, m);
-            switch (d) {                            // push B (static register slots / LDS rows)
+        for (int w = 0; w < 32; ++w) {
+            X[w] = rp_a(L[w], R[w], sh, m);
+            B[w] = rp_b(L[w], R[w], sh, m);
+        }
+        const uint32_t tB = rp_b(tL, tR, sh, m);
+        tX = rp_a(tL, tR, sh, m);
+        path <<= 1;
+        if (d + 1 < kBsD) {
+            switch (d) {                            // push B (static register slots)
                 case 0: DPF_BS_PUSH_LDS(0, B) tS0 = tB; break;
                 case 1: DPF_BS_PUSH_LDS(1, B) tS1 = tB; break;
-                case 2: DPF_BS_COPY(S2, B) tS2 = tB; break;
-                default: DPF_BS_COPY(S3, B) tS3 = tB; break;
+                default: DPF_BS_COPY(S2, B) tS2 = tB; break;
             }
             ++d;
-            path <<= 1;
-            phase = d < kBsD ? 0 : 2;
             continue;
         }
-        // Leaf set: 8 consecutive leaves 8*path + sigma(i) (dpf.go:214-224).
-#pragma unroll
-        for (int w = 0; w < 32; ++w) O[w] = __builtin_amdgcn_bitop3_b32(O[w], tX, fcw[w], 0x78);
-        transpose32(O);
+        // Leaf sets A (X) and B: 8 consecutive leaves 8*path + sigma(i) each (dpf.go:214-224).
         {
-            uint8_t* p = obase + (uint64_t)path * 128;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-                *reinterpret_cast<uint4*>(p + 16 * kBsSigmaLeaf[i]) = make_uint4(O[i], O[8 + i], O[16 + i], O[24 + i]);
+            uint32_t O[32];
+            aes_mmo8(X, O, 0);
+            leaf_store(O, tX, fcw, obase + (uint64_t)path * 128);
         }
-        while (d > 0 && (path & 1u)) {          // climb over finished right branches
+        {
+            uint32_t O[32];
+            aes_mmo8(B, O, 0);
+            leaf_store(O, tB, fcw, obase + (uint64_t)(path + 1) * 128);
+        }
+        path >>= 1;                               // back to X's own index at depth d
+        while (d > 0 && (path & 1u)) {            // climb over finished right branches
             path >>= 1;
             --d;
         }
         if (d == 0) break;
-        switch (d - 1) {                        // pop the pending right set of depth d-1
+        switch (d - 1) {                        // pop the pending right set of depth d
             case 0: DPF_BS_POP_LDS(0, X) tX = tS0; break;
             case 1: DPF_BS_POP_LDS(1, X) tX = tS1; break;
-            case 2: DPF_BS_COPY(X, S2) tX = tS2; break;
-            default: DPF_BS_COPY(X, S3) tX = tS3; break;
+            default: DPF_BS_COPY(X, S2) tX = tS2; break;
         }
         path |= 1u;
-        phase = d < kBsD ? 0 : 2;
     }
 }
 
