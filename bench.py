@@ -220,6 +220,8 @@ class Ctx:
         self.dev = torch.device("cuda", self.local)
         torch.cuda.set_device(self.dev)
         dpf.gpu_init_devices([self.local])      # this rank's GPU only: no context on the others
+        if args.aes:
+            dpf.set_aes_impl(args.aes)
         self.stream = torch.cuda.current_stream(self.dev)
 
     def timed(self, step, steps, warmup):
@@ -278,8 +280,6 @@ def wl_evalfull(c: Ctx) -> dict:
             ev[1].record(c.stream)
 
     names = {dpf.AES_TTABLE: "lds-ttable", dpf.AES_BITSLICED: "bitsliced"}
-    if a.aes:
-        dpf.set_aes_impl(a.aes)
     main_impl = dpf.get_aes_impl()
     t_wall, k_ms = c.timed(step, a.steps, a.warmup)
     sec = t_wall / a.steps
@@ -449,6 +449,7 @@ def wl_pir(c: Ctx) -> dict:
                   value=nk / sec, unit="queries/s", ms_per_step=sec * 1e3, scaling="strong",
                   data="synthetic DB (SplitMix64) + keys",
                   config={"workload": f"PIR, DB 2^{logN} x 32 B sharded over {W} GPU(s), batch {nk}"
+                                      + f" ({'bitsliced' if dpf.get_aes_impl() else 'lds-ttable'} AES)"
                                       + (" (rank 0's share timed on 1 GPU)" if W != c.world else "")
                                       + " (BASELINE configs[4])", "logN": logN, "batch": nk,
                           "parallelism": f"db-shard x{c.world} + all_gather/XOR"},

@@ -6,9 +6,9 @@
 //
 // Work split (one launch of each):
 //   1. k_evalfull<NODES> (T-table, dpf_kernels.hip) writes the frontier: the
-//      2^f nodes of every key at level f = stop - kBsD (seed + t byte);
-//   2. k_evalfull_bs: a lane takes 8 consecutive frontier nodes as one
-//      byte-sliced set (aes_bytesliced.hpp) and expands them kBsD levels
+//      2^f nodes of every key at level f = stop - D (seed + t byte);
+//   2. k_evalfull_bs<D>: a lane takes 8 consecutive frontier nodes as one
+//      byte-sliced set (aes_bytesliced.hpp) and expands them D levels
 //      depth-first.  An expansion is two AES-MMO sets (all 8 nodes under the
 //      left key, then the right key); the 16 children are repacked into the
 //      next two sets of 8 consecutive nodes with one shift + one v_bitop3 per
@@ -94,13 +94,13 @@ __device__ __forceinline__ uint32_t rp_b(uint32_t l, uint32_t r, uint32_t s, uin
 // Leaf conversion of a set (MMO_L output o, leaf t mask tl): ^ (t ? finalCW :
 // 0), back to 8 blocks, 8 consecutive 16-byte stores (one 128-byte line).
 __device__ __forceinline__ void leaf_store(uint32_t (&o)[32], uint32_t tl, const uint32_t* __restrict__ fcw,
-                                           uint8_t* p) {
+                                           uint8_t* p, const Sigma& sig) {
 #pragma unroll
     for (int w = 0; w < 32; ++w) o[w] = __builtin_amdgcn_bitop3_b32(o[w], tl, fcw[w], 0x78);
     transpose32(o);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        *reinterpret_cast<uint4*>(p + 16 * kBsSigmaLeaf[i]) = make_uint4(o[i], o[8 + i], o[16 + i], o[24 + i]);
+        *reinterpret_cast<uint4*>(p + 16 * sig.v[i]) = make_uint4(o[i], o[8 + i], o[16 + i], o[24 + i]);
 }
 
 #define DPF_BS_COPY(DST, SRC) _Pragma("unroll") for (int w_ = 0; w_ < 32; ++w_) DST[w_] = SRC[w_];
@@ -116,9 +116,9 @@ __device__ __forceinline__ void leaf_store(uint32_t (&o)[32], uint32_t tl, const
 constexpr int kBsBlock = 256;
 
 // Thread u: key u >> (flog - 3), frontier nodes 8*(u mod 2^(flog-3)) .. +7
-// of that key (level lvl0; 2^flog frontier nodes per key).  Output: 2^kBsD
+// of that key (level lvl0; 2^flog frontier nodes per key).  Output: 2^D
 // leaves of 16 B below each node, at out + key * out_stride.
-template <bool UNIFORM>
+template <int D, bool UNIFORM>
 __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __restrict__ fseed,
                                                         const uint8_t* __restrict__ ft, uint32_t flog,
                                                         const uint32_t* __restrict__ ekb, uint32_t stop,
@@ -133,7 +133,8 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
     const uint64_t node0 = (key << flog) + 8 * g;
     const uint32_t* ek = ekb + key * bs_key_words(stop);
     const uint32_t* fcw = ek + (uint64_t)stop * kBsRec;
-    uint8_t* obase = out + key * out_stride + ((g * 8) << kBsD) * 16;
+    uint8_t* obase = out + key * out_stride + ((g * 8) << D) * 16;
+    constexpr Sigma sig = sigma_at(D);
 
     uint32_t X[32];
 #pragma unroll
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
         tX *= 0x01010101u;
     }
 
-    // Depth-first over sets.  An iteration expands X (depth d < kBsD, set
+    // Depth-first over sets.  An iteration expands X (depth d < D, set
     // index `path` among the 2^d sets of the lane at that depth): left and
     // right AES-MMO sets, repack into A (first 8 children) and B (last 8).
     // Above the leaves A is expanded next and B waits in a stack slot; at
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
         const uint32_t tB = rp_b(tL, tR, sh, m);
         tX = rp_a(tL, tR, sh, m);
         path <<= 1;
-        if (d + 1 < kBsD) {
+        if (d + 1 < D) {
             switch (d) {                            // push B (static register slots)
                 case 0: DPF_BS_PUSH_LDS(0, B) tS0 = tB; break;
                 case 1: DPF_BS_PUSH_LDS(1, B) tS1 = tB; break;
@@ -200,12 +201,12 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
         {
             uint32_t O[32];
             aes_mmo8(X, O, 0);
-            leaf_store(O, tX, fcw, obase + (uint64_t)path * 128);
+            leaf_store(O, tX, fcw, obase + (uint64_t)path * 128, sig);
         }
         {
             uint32_t O[32];
             aes_mmo8(B, O, 0);
-            leaf_store(O, tB, fcw, obase + (uint64_t)(path + 1) * 128);
+            leaf_store(O, tB, fcw, obase + (uint64_t)(path + 1) * 128, sig);
         }
         path >>= 1;                               // back to X's own index at depth d
         while (d > 0 && (path & 1u)) {            // climb over finished right branches
@@ -232,13 +233,36 @@ hipError_t launch_unpack_bs(const uint8_t* keys, uint64_t key_len, uint64_t nkey
 }
 
 bool bs_applicable(uint32_t stop, uint32_t prefix_bits) {
-    return stop >= prefix_bits + kBsD + 3;   // >= 8 frontier nodes per key below the prefix
+    return stop >= prefix_bits + kBsDMin + 3;   // >= 8 frontier nodes per key below the prefix
 }
 
+// Lanes of depth 4 when that fills 2 waves/SIMD on every CU, else depth 3
+// (twice the lanes, a frontier one level deeper).
+uint32_t bs_depth(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits) {
+    if (stop < prefix_bits + kBsDMax + 3) return kBsDMin;
+    const uint64_t lanes4 = nkeys << (stop - prefix_bits - kBsDMax - 3);
+    return lanes4 >= 131072 ? kBsDMax : kBsDMin;
+}
+
+// Sized for the shallower depth (the larger frontier) whatever is picked per launch.
 uint64_t bs_frontier_bytes(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits) {
     if (!bs_applicable(stop, prefix_bits)) return 0;
-    const uint64_t n = nkeys << (stop - kBsD - prefix_bits);
+    const uint64_t n = nkeys << (stop - kBsDMin - prefix_bits);
     return (n * 16 + n + 255) & ~255ull;
+}
+
+template <int D>
+static hipError_t launch_bs_d(const uint4* fs, const uint8_t* fts, uint32_t flog, const uint32_t* ekb, uint32_t stop,
+                              uint32_t f, uint64_t nkeys, uint8_t* out, uint64_t out_stride, hipStream_t st) {
+    const uint64_t threads = nkeys << (flog - 3);
+    const dim3 grid((uint32_t)((threads + kBsBlock - 1) / kBsBlock));
+    if (flog - 3 >= 6)
+        hipLaunchKernelGGL((k_evalfull_bs<D, true>), grid, dim3(kBsBlock), 0, st, fs, fts, flog, ekb, stop, f, threads,
+                           out, out_stride);
+    else
+        hipLaunchKernelGGL((k_evalfull_bs<D, false>), grid, dim3(kBsBlock), 0, st, fs, fts, flog, ekb, stop, f,
+                           threads, out, out_stride);
+    return hipGetLastError();
 }
 
 hipError_t launch_evalfull_bs(const uint32_t* ek, const uint32_t* ekb, uint64_t nkeys, uint32_t stop,
@@ -246,21 +270,16 @@ hipError_t launch_evalfull_bs(const uint32_t* ek, const uint32_t* ekb, uint64_t 
                               hipStream_t st) {
     if (nkeys == 0) return hipSuccess;
     if (!bs_applicable(stop, prefix_bits)) return hipErrorInvalidValue;
-    const uint32_t f = stop - kBsD;                 // frontier level
+    const uint32_t dd = bs_depth(nkeys, stop, prefix_bits);
+    const uint32_t f = stop - dd;                   // frontier level
     const uint32_t flog = f - prefix_bits;          // frontier nodes per key below the prefix
     uint8_t* fs = static_cast<uint8_t*>(frontier);
     uint8_t* fts = fs + (nkeys << flog) * 16;
     hipError_t e = launch_nodes(ek, nkeys, stop, f, prefix_bits, prefix, fs, fts, 1ull << flog, st);
     if (e != hipSuccess) return e;
-    const uint64_t threads = nkeys << (flog - 3);
-    const dim3 grid((uint32_t)((threads + kBsBlock - 1) / kBsBlock));
-    if (flog - 3 >= 6)
-        hipLaunchKernelGGL(k_evalfull_bs<true>, grid, dim3(kBsBlock), 0, st, reinterpret_cast<const uint4*>(fs), fts, flog,
-                           ekb, stop, f, threads, out, out_stride);
-    else
-        hipLaunchKernelGGL(k_evalfull_bs<false>, grid, dim3(kBsBlock), 0, st, reinterpret_cast<const uint4*>(fs), fts,
-                           flog, ekb, stop, f, threads, out, out_stride);
-    return hipGetLastError();
+    const uint4* fsv = reinterpret_cast<const uint4*>(fs);
+    return dd == kBsDMax ? launch_bs_d<kBsDMax>(fsv, fts, flog, ekb, stop, f, nkeys, out, out_stride, st)
+                         : launch_bs_d<kBsDMin>(fsv, fts, flog, ekb, stop, f, nkeys, out, out_stride, st);
 }
 
 // 8 independent blocks per lane through the byte-sliced MMO (AES

@@ -5,7 +5,10 @@
 
 namespace dpfk {
 
-constexpr uint32_t kBsD = 4;   // levels a lane expands below the frontier (2^kBsD leaves per node)
+// Levels a lane expands below the frontier (2^D leaves per node): 4, or 3
+// when 4 would leave CUs idle (bs_depth).
+constexpr uint32_t kBsDMax = 4;
+constexpr uint32_t kBsDMin = 3;
 
 // Block order inside a set of 8 consecutive nodes: after an expansion at
 // depth d (shift s_d = 4, 2, 1 cycling, P_d = {p : (p & s_d) == 0}), block p
@@ -27,7 +30,6 @@ constexpr Sigma sigma_at(uint32_t depth) {
     }
     return s;
 }
-constexpr Sigma kBsSigma = sigma_at(kBsD);
 constexpr bool sigma_ok(uint32_t depth) {
     for (uint32_t d = 0; d <= depth; ++d)
         for (uint32_t p = 0; p < 8; ++p)
@@ -35,11 +37,12 @@ constexpr bool sigma_ok(uint32_t depth) {
     return true;
 }
 static_assert(sigma_ok(12), "set block order invariant");
-static_assert(kBsSigma.v[0] == 0 && kBsSigma.v[1] == 2 && kBsSigma.v[4] == 1, "sigma(4) = [0,2,4,6,1,3,5,7]");
-#define kBsSigmaLeaf (::dpfk::kBsSigma.v)
+static_assert(sigma_at(4).v[0] == 0 && sigma_at(4).v[1] == 2 && sigma_at(4).v[4] == 1, "sigma(4) = [0,2,4,6,1,3,5,7]");
+static_assert(sigma_at(3).v[5] == 5, "sigma(3) = identity");
 
 __host__ __device__ uint64_t bs_key_words(uint32_t stop);   // byte-sliced correction words per key
 bool bs_applicable(uint32_t stop, uint32_t prefix_bits);
+uint32_t bs_depth(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits);
 uint64_t bs_frontier_bytes(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits);
 
 hipError_t launch_unpack_bs(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ekb,

@@ -157,9 +157,12 @@ class CopyPool {
     void loop() {
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            cv_.wait(lk, [&] { return stop_ || pending() != nullptr; });
+            // Take the job the predicate found, under the same lock hold: the
+            // piece counter (`next`) moves without the lock, so a second
+            // pending() call could find the job already exhausted.
+            Job* j = nullptr;
+            cv_.wait(lk, [&] { return stop_ || (j = pending()) != nullptr; });
             if (stop_) return;
-            Job* j = pending();
             ++j->active;
             lk.unlock();
             run(*j);
@@ -333,17 +336,6 @@ hipError_t run_tree(const TreeWs& w, size_t k0, size_t n, uint32_t stop, uint32_
         return dpfk::launch_evalfull_bs(w.ek + k0 * dpfk::ek_words(stop), w.ekb + k0 * dpfk::bs_key_words(stop), n, stop,
                                         prefix_bits, prefix, out, stride, w.frontier, st);
     return dpfk::launch_evalfull(w.ek + k0 * dpfk::ek_words(stop), n, stop, prefix_bits, prefix, out, stride, st);
-}
-
-// Evaluate subtree (prefix_bits, prefix) of nk keys already resident at
-// d_keys into d_out (2^(stop-prefix_bits) leaves per key), on stream st.
-int enqueue_full(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t logN, uint32_t prefix_bits,
-                 uint64_t prefix, uint8_t* d_out, uint32_t* d_work, hipStream_t st) {
-    const uint32_t stop = stop_of(logN);
-    HIP_TRY(dpfk::launch_unpack(d_keys, klen, nk, stop, d_work, st));
-    const uint64_t stride = (uint64_t)16 << (stop - prefix_bits);
-    HIP_TRY(dpfk::launch_evalfull(d_work, nk, stop, prefix_bits, prefix, d_out, stride, st));
-    return DPF_OK;
 }
 
 // Pipelined device -> host output of `nchunks` chunks (<= chunk_cap bytes
@@ -739,7 +731,8 @@ int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint
 size_t dpf_pir_workspace_size(size_t nkeys, uint32_t logN, uint32_t prefix_bits) {
     const uint32_t stop = stop_of(logN);
     const uint32_t pb = prefix_bits > stop ? stop : prefix_bits;
-    return pir_ek_bytes(nkeys, logN) + nkeys * ((size_t)16 << (stop - pb)) + dpfk::pir_fold_parts_bytes();
+    return align256(tree_ws_bytes(nkeys, stop, pb, nkeys)) + align256(nkeys * ((size_t)16 << (stop - pb))) +
+           dpfk::pir_fold_parts_bytes();
 }
 
 int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN,
@@ -754,12 +747,13 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     hipStream_t st = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(d_ans, 0, nkeys * 32, st));
     if (nkeys == 0 || nrec == 0) return DPF_OK;
-    uint32_t* ek = (uint32_t*)d_work;
-    uint8_t* bits = (uint8_t*)d_work + pir_ek_bytes(nkeys, logN);
+    // [tree workspace | selection bits = EvalFull bytes of the subtree | fold partials]
+    const TreeWs w = tree_ws(d_work, nkeys, stop);
+    uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
     const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
-    int rc = enqueue_full(d_keys, klen, nkeys, logN, prefix_bits, prefix, bits, ek, st);
-    if (rc) return rc;
-    uint32_t* parts = (uint32_t*)(bits + nkeys * per_key);
+    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st));
+    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st));
+    uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
     HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, (uint32_t)nkeys, (uint32_t*)d_ans, parts,
                                   st));
     return DPF_OK;

@@ -190,6 +190,39 @@ static void gpu_checks(void) {
         CHECK(ones == 1 && bit(o, 0xABCDE) != bit(o + ol2, 0xABCDE), "point function at logN=24");
         free(k2a); free(k2b); free(o);
     }
+    /* Multi-chunk batched Eval right after EvalFull re-sized the staging
+     * buffers: the CopyPool handing 2 MiB pieces of the xs / result copies to
+     * its workers (a worker once took a job another thread had just
+     * exhausted and dereferenced null). */
+    {
+        const uint32_t L = 20;
+        const size_t nk = 16384, ppk = 1024, kl3 = dpf_key_len(L);
+        uint8_t* k3 = malloc(nk * kl3);
+        uint8_t* k3b = malloc(nk * kl3);
+        uint64_t* al = malloc(nk * 8);
+        uint8_t* sd = malloc(nk * 32);
+        uint64_t* xs = malloc(nk * ppk * 8);
+        uint8_t* ea = malloc(nk * ppk);
+        uint8_t* eb = malloc(nk * ppk);
+        uint8_t* full = malloc(64 * dpf_evalfull_len(L));
+        for (size_t i = 0; i < nk; ++i) {
+            al[i] = (i * 2654435761u) & ((1u << L) - 1);
+            for (int q = 0; q < 32; ++q) sd[32 * i + q] = (uint8_t)(i * 13 + q);
+            for (size_t q = 0; q < ppk; ++q) xs[i * ppk + q] = q == 5 ? al[i] : ((i * 7919 + q * 104729) & ((1u << L) - 1));
+        }
+        CHECK(dpf_gen_batch_seeded(al, L, sd, sd + 16, nk, k3, k3b, 0) == DPF_OK, "gen");
+        for (int rep = 0; rep < 3; ++rep) {
+            CHECK(dpf_evalfull_batch(k3, kl3, 64, L, full, 1) == DPF_OK, "evalfull before eval");
+            CHECK(dpf_eval_batch(k3, kl3, nk, xs, ppk, L, ea, 1) == DPF_OK, "eval a");
+            CHECK(dpf_eval_batch(k3b, kl3, nk, xs, ppk, L, eb, 1) == DPF_OK, "eval b");
+            for (size_t i = 0; i < nk; i += 97)
+                for (size_t q = 0; q < ppk; ++q)
+                    CHECK((ea[i * ppk + q] ^ eb[i * ppk + q]) == (xs[i * ppk + q] == al[i]), "eval shares");
+            for (size_t i = 0; i < 64; ++i)
+                CHECK(bit(full + i * dpf_evalfull_len(L), xs[i * ppk + 7]) == ea[i * ppk + 7], "eval vs evalfull");
+        }
+        free(k3); free(k3b); free(al); free(sd); free(xs); free(ea); free(eb); free(full);
+    }
     dpf_gpu_shutdown();
 }
 

@@ -40,10 +40,10 @@ def test_sizes():
         stop = max(logN - 7, 0)
         assert dpf.key_len(logN) == 33 + 18 * stop
         assert dpf.evalfull_len(logN) == (16 if logN < 7 else 1 << (logN - 3))
-    # T-table records + byte-sliced CW words + byte-sliced frontier (2^9 nodes x 17 B per key)
+    # T-table records + byte-sliced CW words + byte-sliced frontier (up to 2^10 nodes x 17 B per key)
     al = lambda x: (x + 255) // 256 * 256
     assert dpf.workspace_size(4096, 20) == (al(4096 * (13 + 2) * 32) + al(4096 * (13 * 36 + 32) * 4)
-                                            + al(4096 * 512 * 17))
+                                            + al(4096 * 1024 * 17))
 
 
 def test_host_gen_matches_golden():

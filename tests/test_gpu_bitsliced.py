@@ -127,3 +127,16 @@ def test_subtree_slices_and_split_bitsliced():
             torch.cuda.synchronize()
             assert np.array_equal(d_part.cpu().numpy().reshape(nk, part), host[:, p * part:(p + 1) * part]), (pb, p)
     assert dpf.evalfull_split(ka[0].tobytes(), logN, 1).tobytes() == host[0].tobytes()
+
+
+@pytest.mark.parametrize("logN,nrec,nk", [(14, 16384, 9), (16, 50000, 70)])
+def test_pir_bitsliced_vs_oracle(logN, nrec, nk):
+    """PIR answers with the byte-sliced tree producing the selection bits."""
+    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    _, ka, _ = _keys(nk, logN, first=logN + 5)
+    pdb = dpf.PirDB(db, logN, ngpus=1)
+    got = pdb.answer(ka)
+    pdb.close()
+    want = np.stack([np.frombuffer(oracle.pir_answer(ka[i].tobytes(), logN, db, 0, nrec), np.uint8)
+                     for i in range(nk)])
+    assert np.array_equal(got, want)

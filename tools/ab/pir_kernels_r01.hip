@@ -13,7 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "pir_kernels.hpp"
+#include "../../dpf-go_amd/csrc/pir_kernels.hpp"
 
 namespace dpfk {
 
@@ -22,59 +22,55 @@ namespace dpfk {
 // ans[64 keys][256 bits] = S[64 x n] . DB[n x 256]; done as 8 masked XORs per
 // (key, record) it is VALU-bound at 8 n B lane-ops.  Here a wave takes 64
 // records (a "chunk") x 64 keys (lane = key) at a time:
-//   load  : the chunk's 2 KiB as two fully coalesced 1 KiB wave loads (each
-//           16-B piece of the DB is requested exactly once), staged to the
-//           wave's LDS area with two conflict-free 1 KiB stores;
-//   build : group g = records 4g .. 4g+3; its 16 table entries (entry e =
-//           XOR of the records whose bit is set in e) are built by lanes
-//           4g .. 4g+3: lane j reads half h = j&1 of the group's 4 records
-//           from the staged chunk and writes entries 8a + k (a = j>>1) of
-//           that half, 16 B each, over the staged chunk (a wave's LDS
-//           operations complete in order, so its own reads come first);
-//   lookup: each key-lane takes the group's 4 selection bits -- nibble g of
-//           its 64 selection bits, exactly EvalFull's LSB-first layout --
-//           as the entry index and XORs the 32-byte entry (2 ds_read_b128)
-//           into its accumulator: 8 XORs per 4 records instead of 32, done
-//           as 3-input XORs over two groups.
-// Table rows (group g, half h) of 16 slots x 16 B; entry e sits in slot
-// e ^ (e >> 3) ^ (4*(g&1) + 2*h).  A lookup (ds_read_b128, 16-lane passes
-// over 64 banks) reads one row: distinct entries hit distinct bank groups,
-// equal ones broadcast.  A build store (ds_write_b128, 8-lane passes over
-// 32 banks) comes from lanes whose (g&1, h, a) differ: 8 distinct slots
-// mod 8.  Lanes are keys, so there is no cross-lane reduction: the
-// workgroup's waves combine in LDS into one 64 x 32-byte partial and
-// k_xor_parts folds those.  The 8 waves of a workgroup take interleaved
-// chunks of one contiguous range, so each 128-B line of a key's selection
-// bits is staged once per 16 chunks.
-constexpr int kM4Waves = 8;          // waves per workgroup (8 KiB of LDS each)
+//   build : each of the chunk's 16 groups of 4 records gets a 16-entry table
+//           of all XOR combinations (entry e = XOR of the records b with bit b
+//           of e set), built in registers by the 4 lanes of a quad (DPP quad
+//           broadcasts) and stored to a wave-private LDS table (8 KiB);
+//   lookup: each key-lane uses its 4 selection bits of a group as the entry
+//           index and XORs the 32-byte entry (2 ds_read_b128) into its
+//           accumulator: 8 XORs per 4 records instead of 32.
+// Lanes are keys, so there is no cross-lane reduction: the workgroup's waves
+// combine in LDS into one 64 x 32-byte partial and k_xor_parts folds those.
+// The 8 waves of a workgroup take interleaved chunks of one contiguous range,
+// so each 128-B line of a key's selection bits is consumed by the workgroup
+// within two iterations (L1-resident) rather than by one wave over 16.
+// LDS layout of a wave's table: [group 16][half 2][slot 16] x 16 B, entry e of
+// group g in slot pi(e) ^ (g & 1), pi(e) = e ^ ((e >> 2) & 2).  A lookup reads
+// one (group, half) row of 256 B: distinct entries hit distinct banks (b128:
+// bank (a/4) mod 64), equal ones broadcast.  The build stores lane (quad q,
+// position p) entry 4p + j; pi makes the 8 lanes of each b128 store group hit
+// 8 distinct 16-B bank groups (stores: bank (a/4) mod 32).
+#ifndef DPF_FOLD_EXP
+#define DPF_FOLD_EXP 0   // measurement knob (tools/fold_bench.hip): 1 no table stores, 2 no lookups, 3 no record loads
+#endif
+constexpr int kM4Waves = 8;          // waves per workgroup (8 KiB of LDS table each)
 constexpr int kM4Groups = 16;        // 4-record groups per 64-record chunk
 constexpr int kM4MaxKeys = 64;       // keys per launch (one per lane)
-constexpr int kSelRow = 34;          // staged selection row: 32 words + pad -> conflict-free ds_read_b64
+constexpr int kSelRow = 36;          // staged selection row: 32 words + pad (2-way ds_read_b64)
 
-__device__ __forceinline__ uint4 x4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
-__device__ __forceinline__ uint4 x4_3(uint4 a, uint4 b, uint4 c) {
-    return make_uint4(__builtin_amdgcn_bitop3_b32(a.x, b.x, c.x, 0x96), __builtin_amdgcn_bitop3_b32(a.y, b.y, c.y, 0x96),
-                      __builtin_amdgcn_bitop3_b32(a.z, b.z, c.z, 0x96), __builtin_amdgcn_bitop3_b32(a.w, b.w, c.w, 0x96));
+template <int SRC>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t x) {
+    // quad_perm [SRC, SRC, SRC, SRC]
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, SRC * 0x55, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
+
+__device__ __forceinline__ uint32_t m4_slot(uint32_t e, uint32_t g) { return e ^ ((e >> 2) & 2u) ^ (g & 1u); }
 
 __global__ __launch_bounds__(64 * kM4Waves, 4) void k_pir_fold4r(const uint32_t* __restrict__ bits, uint64_t wpk,
                                                               const uint4* __restrict__ db, uint64_t nrec,
                                                               uint32_t nkeys, uint64_t chunks_per_block,
                                                               uint32_t* __restrict__ parts) {
     __shared__ uint4 s_tab[kM4Waves][kM4Groups * 2 * 16];
-    __shared__ __attribute__((aligned(16))) uint32_t s_sel[kM4MaxKeys * kSelRow];
+    __shared__ __attribute__((aligned(16))) uint32_t s_sel[kM4MaxKeys][kSelRow];
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t nchunks = (nrec + 63) / 64;
     const uint64_t c0 = (uint64_t)blockIdx.x * chunks_per_block;
     const uint64_t cend = c0 + chunks_per_block < nchunks ? c0 + chunks_per_block : nchunks;
-    // Lanes past nkeys read key 0's bits and mask them off; loads past the
-    // last record re-read the last record (selection bits are masked).
+    // Lanes past nkeys read key 0's bits and mask them off; lanes past the
+    // last record read the last record and the selection bits are masked.
     const uint32_t keymask = l < nkeys ? ~0u : 0u;
     // Selection-bit staging: thread t copies 16 B of key t/8's 128-B line
-    // (16 chunks) per batch into row t/8 (two 8-byte stores).
+    // (16 chunks) per batch; rows padded to kSelRow words.
     const uint32_t sk = threadIdx.x >> 3, sp = threadIdx.x & 7;
     const uint32_t* srow = bits + (uint64_t)(sk < nkeys ? sk : 0) * wpk;
     auto load_sel = [&](uint64_t cb) {
@@ -82,64 +78,76 @@ __global__ __launch_bounds__(64 * kM4Waves, 4) void k_pir_fold4r(const uint32_t*
         return wo + 4 <= wpk ? *reinterpret_cast<const uint4*>(srow + wo) : make_uint4(0, 0, 0, 0);
     };
     uint4* tab = s_tab[w];
-    const uint32_t g = l >> 2, j = l & 3, h = j & 1, a = j >> 1;
-    const uint32_t amask = a ? ~0u : 0u;
-    uint4* wrow = tab + (g * 2 + h) * 16;                         // this lane's build row
-    const uint32_t wsw = (4 * (g & 1) + 2 * h) ^ a;              // slot of entry 8a + k: (8a + k) ^ wsw
-    const uint4* grec = tab + 8 * g + h;                          // staged half h of record 4g (+2 per record)
+    const uint32_t q = l >> 2, p = l & 3;
+    const uint32_t m2 = (p & 1) ? ~0u : 0u, m3 = (p & 2) ? ~0u : 0u;
     uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // The chunk's 2 KiB: lane l gets bytes [16l, 16l+16) of each 1 KiB half.
-    auto load = [&](uint64_t cc, uint4& A, uint4& B) {
+    // Chunk cc's record (lane l) and selection words; branch-free so the
+    // loads of the next chunk stay in flight while this one is folded.
+    auto load = [&](uint64_t cc, uint4& a, uint4& b) {
         if (cc >= nchunks) cc = nchunks - 1;
-        uint64_t ra = cc * 64 + (l >> 1), rb = ra + 32;
-        if (ra >= nrec) ra = nrec - 1;
-        if (rb >= nrec) rb = nrec - 1;
-        A = db[2 * ra + (l & 1)];
-        B = db[2 * rb + (l & 1)];
+        uint64_t r = cc * 64 + l;
+        if (r >= nrec) r = nrec - 1;
+#if DPF_FOLD_EXP == 3
+        a = make_uint4((uint32_t)r, (uint32_t)r * 3u, (uint32_t)r * 5u, (uint32_t)r * 7u);
+        b = make_uint4((uint32_t)r * 9u, (uint32_t)r * 11u, (uint32_t)r * 13u, (uint32_t)r * 15u);
+#else
+        a = db[2 * r];
+        b = db[2 * r + 1];
+#endif
     };
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    auto fold = [&](uint64_t cc, uint64_t cb, const uint4& A, const uint4& B) {
-        tab[l] = A;                                 // staged chunk: record r half hh at 16-B slot 2r + hh
-        tab[64 + l] = B;
-        wave_sync();
-        const uint4 R0 = grec[0], R1 = grec[2], R2 = grec[4], R3 = grec[6];
-        wave_sync();
-        // entries 8a + k = (XOR of R0/R1/R2 by the bits of k) ^ (a ? R3 : 0)
-        const uint4 R3m = make_uint4(R3.x & amask, R3.y & amask, R3.z & amask, R3.w & amask);
-        const uint4 R01 = x4(R0, R1);
-        const uint32_t b8 = 8 * a;
-        wrow[(b8 + 0) ^ wsw] = R3m;
-        wrow[(b8 + 1) ^ wsw] = x4(R0, R3m);
-        wrow[(b8 + 2) ^ wsw] = x4(R1, R3m);
-        wrow[(b8 + 3) ^ wsw] = x4(R01, R3m);
-        wrow[(b8 + 4) ^ wsw] = x4(R2, R3m);
-        wrow[(b8 + 5) ^ wsw] = x4_3(R2, R0, R3m);
-        wrow[(b8 + 6) ^ wsw] = x4_3(R2, R1, R3m);
-        wrow[(b8 + 7) ^ wsw] = x4_3(R01, R2, R3m);
-        wave_sync();
-        uint2 sel = *reinterpret_cast<const uint2*>(&s_sel[l * kSelRow + 2 * (cc - cb)]);
+    // Fold chunk cc (record words x, selection words sel) into acc.
+    auto fold = [&](uint64_t cc, uint64_t cb, const uint4& ra, const uint4& rb) {
+        const uint32_t x[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+        uint2 sel = *reinterpret_cast<const uint2*>(&s_sel[l][2 * (cc - cb)]);
         const uint64_t valid = cc < cend ? nrec - cc * 64 : 0;   // records of this chunk below nrec
         sel.x &= keymask & (valid >= 32 ? ~0u : (1u << valid) - 1u);
         sel.y &= keymask & (valid >= 64 ? ~0u : valid <= 32 ? 0u : (1u << (valid - 32)) - 1u);
-        // Pre-swizzle the nibbles: slot = e ^ (e >> 3) ^ 4 (odd groups); the half-1 slot is that ^ 2.
-        const uint32_t zx = sel.x ^ ((sel.x >> 3) & 0x11111111u) ^ 0x40404040u;
-        const uint32_t zy = sel.y ^ ((sel.y >> 3) & 0x11111111u) ^ 0x40404040u;
+        // Build: lane p of quad q computes entries 4p + j (j < 4) of group q,
+        // E = A[j] ^ B[p] with A = {0, r0, r1, r0^r1}, B = {0, r2, r3, r2^r3};
+        // one 16-byte half at a time.
 #pragma unroll
-        for (int gg = 0; gg < kM4Groups; gg += 2) {
-            const uint32_t z = gg < 8 ? zx : zy;
-            const uint32_t s0 = (z >> (4 * (gg & 7))) & 15u, s1 = (z >> (4 * ((gg + 1) & 7))) & 15u;
-            const uint4 lo0 = tab[(gg * 2 + 0) * 16 + s0], hi0 = tab[(gg * 2 + 1) * 16 + (s0 ^ 2)];
-            const uint4 lo1 = tab[(gg * 2 + 2) * 16 + s1], hi1 = tab[(gg * 2 + 3) * 16 + (s1 ^ 2)];
-            acc[0] = x3(acc[0], lo0.x, lo1.x); acc[1] = x3(acc[1], lo0.y, lo1.y);
-            acc[2] = x3(acc[2], lo0.z, lo1.z); acc[3] = x3(acc[3], lo0.w, lo1.w);
-            acc[4] = x3(acc[4], hi0.x, hi1.x); acc[5] = x3(acc[5], hi0.y, hi1.y);
-            acc[6] = x3(acc[6], hi0.z, hi1.z); acc[7] = x3(acc[7], hi0.w, hi1.w);
+        for (int h = 0; h < 2; ++h) {
+            uint32_t e[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t xi = x[4 * h + i];
+                const uint32_t r0 = quad_bcast<0>(xi), r1 = quad_bcast<1>(xi);
+                const uint32_t r2 = quad_bcast<2>(xi), r3 = quad_bcast<3>(xi);
+                const uint32_t bp = __builtin_amdgcn_bitop3_b32(r2, m2, r3 & m3, 0x6a);   // (r2 & m2) ^ c
+                e[0][i] = bp;
+                e[1][i] = r0 ^ bp;
+                e[2][i] = r1 ^ bp;
+                e[3][i] = __builtin_amdgcn_bitop3_b32(r0, r1, bp, 0x96);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (DPF_FOLD_EXP == 1 && e[j][0] != 0x12345678u) continue;
+                tab[(q * 2 + h) * 16 + m4_slot(4 * p + j, q)] = make_uint4(e[j][0], e[j][1], e[j][2], e[j][3]);
+            }
         }
-        wave_sync();
+        // LDS operations of one wave complete in order: once the compiler
+        // keeps program order (wavefront-scope fence), the lookups below see
+        // the whole table and the next chunk's stores follow these reads.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if DPF_FOLD_EXP == 2
+        acc[0] ^= sel.x; acc[1] ^= sel.y;
+#pragma unroll
+        for (int g = 0; g < 0; ++g) {
+#else
+#pragma unroll
+        for (int g = 0; g < kM4Groups; ++g) {
+#endif
+            const uint32_t word = g < 8 ? sel.x : sel.y;
+            const uint32_t slot = m4_slot((word >> (4 * (g & 7))) & 15u, g);
+            const uint4 lo = tab[(g * 2 + 0) * 16 + slot], hi = tab[(g * 2 + 1) * 16 + slot];
+            acc[0] ^= lo.x; acc[1] ^= lo.y; acc[2] ^= lo.z; acc[3] ^= lo.w;
+            acc[4] ^= hi.x; acc[5] ^= hi.y; acc[6] ^= hi.z; acc[7] ^= hi.w;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     // Batches of 16 chunks (one 128-B line of every key's selection bits);
     // each wave folds chunks cb + w and cb + 8 + w of a batch.  Record loads
@@ -150,8 +158,7 @@ __global__ __launch_bounds__(64 * kM4Waves, 4) void k_pir_fold4r(const uint32_t*
     uint4 snext = c0 < cend ? load_sel(c0) : make_uint4(0, 0, 0, 0);
     for (uint64_t cb = c0; cb < cend; cb += 2 * kM4Waves) {
         __syncthreads();                                  // previous batch's selection reads are done
-        *reinterpret_cast<uint2*>(&s_sel[sk * kSelRow + 4 * sp]) = make_uint2(snext.x, snext.y);
-        *reinterpret_cast<uint2*>(&s_sel[sk * kSelRow + 4 * sp + 2]) = make_uint2(snext.z, snext.w);
+        *reinterpret_cast<uint4*>(&s_sel[sk][4 * sp]) = snext;
         __syncthreads();
         if (cb + 2 * kM4Waves < cend) snext = load_sel(cb + 2 * kM4Waves);
         const uint64_t c = cb + w;

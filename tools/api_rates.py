@@ -24,6 +24,10 @@ sys.path.insert(0, os.path.join(ROOT, "dpf-go_amd"))
 import numpy as np  # noqa: E402
 
 
+def mark(msg):
+    print(f"[api_rates] {msg}", file=sys.stderr, flush=True)
+
+
 def med_time(fn, reps=7, warm=2):
     for _ in range(warm):
         fn()
@@ -44,6 +48,7 @@ def main():
     st = torch.cuda.current_stream(dev)
     res = {"device": torch.cuda.get_device_name(0)}
 
+    mark("host api cfg2")
     # ---- host API, cfg 2: 4096 keys x logN=20 EvalFull -> 512 MiB to host
     logN, nk = 20, 4096
     al, s0, s1 = synth.key_seeds(nk, logN)
@@ -51,7 +56,12 @@ def main():
     t = med_time(lambda: dpf.evalfull_batch(ka, logN, ngpus=1), reps=5)
     out_b = nk * dpf.evalfull_len(logN)
     res["host_api"] = {"evalfull_batch_cfg2": {"s": t, "points_per_s": nk * (1 << logN) / t,
-                                               "D2H_GBs": out_b / t / 1e9}}
+                                               "D2H_GBs": out_b / t / 1e9, "out": "fresh array per call"}}
+    reuse = np.empty((nk, dpf.evalfull_len(logN)), np.uint8)
+    t = med_time(lambda: dpf.evalfull_batch(ka, logN, ngpus=1, out=reuse), reps=5)
+    res["host_api"]["evalfull_batch_cfg2_reused_out"] = {"s": t, "points_per_s": nk * (1 << logN) / t,
+                                                         "D2H_GBs": out_b / t / 1e9}
+    mark("cfg3")
     # cfg 3: 2^16 keys x 2^10 points
     ek, ppk = 1 << 16, 1 << 10
     al3, s03, s13 = synth.key_seeds(ek, logN)
@@ -59,11 +69,17 @@ def main():
     xs = synth.eval_points(ek, ppk, logN)
     t = med_time(lambda: dpf.eval_batch(ke, xs, logN, ngpus=1), reps=5)
     res["host_api"]["eval_batch_cfg3"] = {"s": t, "queries_per_s": ek * ppk / t}
+    mark("cfg4")
     # cfg 4: one key logN=32 -> 512 MiB
     al4, s04, s14 = synth.key_seeds(1, 32, first=777)
     k4, _ = dpf.gen_batch_seeded(al4, 32, s04, s14)
     t = med_time(lambda: dpf.evalfull_split(k4[0].tobytes(), 32, 1), reps=3, warm=1)
-    res["host_api"]["evalfull_split_cfg4"] = {"s": t, "points_per_s": (1 << 32) / t}
+    res["host_api"]["evalfull_split_cfg4"] = {"s": t, "points_per_s": (1 << 32) / t, "D2H_GBs": (1 << 29) / t / 1e9}
+    reuse4 = np.empty(1 << 29, np.uint8)
+    t = med_time(lambda: dpf.evalfull_split(k4[0].tobytes(), 32, 1, out=reuse4), reps=3, warm=1)
+    res["host_api"]["evalfull_split_cfg4_reused_out"] = {"s": t, "points_per_s": (1 << 32) / t,
+                                                         "D2H_GBs": (1 << 29) / t / 1e9}
+    mark("cfg5")
     # cfg 5: PIR through the host handle (DB uploaded once)
     pl, B = 24, 64
     db = synth.db_bytes((1 << pl) * 32)
@@ -74,6 +90,7 @@ def main():
     res["host_api"]["pir_answer_cfg5_B64"] = {"s": t, "queries_per_s": B / t}
     del h
 
+    mark("single key")
     # ---- single key (cfg 1), device-resident and host API
     k1 = ka[:1]
     kl = dpf.key_len(logN)
@@ -90,6 +107,7 @@ def main():
     res["single_key_logN20"] = {"evalfull_device_us": t_dev * 1e6, "evalfull_host_api_us": t_host * 1e6,
                                 "eval_one_point_host_api_us": t_eval * 1e6}
 
+    mark("pir sweep")
     # ---- PIR batch sweep (device-resident, like bench.py --workload pir)
     d_db = torch.from_numpy(db).to(dev)
     sweep = {}
@@ -115,6 +133,7 @@ def main():
         sweep[str(b)] = {"ms_per_batch": ms, "queries_per_s": b / (ms * 1e-3)}
     res["pir_batch_sweep_logN24"] = sweep
 
+    mark("gen")
     # ---- host Gen throughput (logN=20 and 32)
     gen = {}
     for gl in (20, 32):

@@ -1,14 +1,16 @@
-// fold_bench.hip — isolates the PIR fold kernel (k_pir_fold4r) at configs[4]
-// shape (2^24 records x 32 B, 64 keys, selection bits as EvalFull writes
-// them) and times it with HIP events.  Built once per DPF_FOLD_EXP variant
-// (tools/exp_fold.sh): 0 full, 1 no table stores, 2 no lookups, 3 no loads.
-// Prints one JSON line.
+// fold_bench.hip — isolates the PIR fold kernel at configs[4] shape (2^24
+// records x 32 B, 64 keys, random selection bits laid out as EvalFull
+// writes them) and times it with HIP events.  Build with -DFOLD_SRC=<file>
+// to A/B another revision of pir_kernels.hip (tools/ab/).  One JSON line.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
 
-#include "../dpf-go_amd/csrc/pir_kernels.hip"
+#ifndef FOLD_SRC
+#define FOLD_SRC "../dpf-go_amd/csrc/pir_kernels.hip"
+#endif
+#include FOLD_SRC
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -18,13 +20,14 @@ int main(int argc, char** argv) {
     const int iters = 20;
     const uint64_t wpk = nrec / 32;
     void *bits, *db, *ans, *parts;
-    CK(hipMalloc(&bits, nkeys * wpk * 4));
+    CK(hipMalloc(&bits, (size_t)nkeys * wpk * 4));
     CK(hipMalloc(&db, nrec * 32));
-    CK(hipMalloc(&ans, nkeys * 32));
+    CK(hipMalloc(&ans, (size_t)nkeys * 32));
     CK(hipMalloc(&parts, dpfk::pir_fold_parts_bytes()));
-    CK(hipMemset(bits, 0x5a, nkeys * wpk * 4));
-    CK(hipMemset(db, 0x3c, nrec * 32));
-    CK(hipMemset(ans, 0, nkeys * 32));
+    std::vector<uint32_t> h((size_t)nkeys * wpk);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)(i * 2654435761u) ^ (uint32_t)(i >> 7);
+    CK(hipMemcpy(bits, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(db, 0x5a, nrec * 32));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -40,7 +43,11 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= iters;
-    printf("{\"exp\": %d, \"nkeys\": %u, \"fold_us\": %.1f, \"GBs\": %.0f}\n", DPF_FOLD_EXP, nkeys, ms * 1e3,
-           (nrec * 32.0 + nkeys * wpk * 4.0) / (ms * 1e-3) / 1e9);
+    std::vector<uint32_t> a((size_t)nkeys * 8);
+    CK(hipMemcpy(a.data(), ans, a.size() * 4, hipMemcpyDeviceToHost));
+    uint32_t chk = 0;
+    for (uint32_t v : a) chk = chk * 31 + v;
+    printf("{\"src\": \"%s\", \"nkeys\": %u, \"fold_us\": %.1f, \"GBs\": %.0f, \"check\": %u}\n", FOLD_SRC, nkeys,
+           ms * 1e3, (nrec * 32 + (double)nkeys * wpk * 4) / (ms * 1e-3) / 1e9, chk);
     return 0;
 }
