@@ -315,7 +315,44 @@ def wl_evalfull(c: Ctx) -> dict:
     line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), kern, k_ms, nk * olen + nk * (stop_of(logN) + 2) * 32,
                                     aes_impl=names[main_impl])
     line["aes_variants"] = variants
+    if c.world == 1 and not a.no_api:
+        line["api"] = api_rates(c, ka, logN)
     return line
+
+
+def api_rates(c: Ctx, ka: np.ndarray, logN: int, reps: int = 5) -> dict:
+    """The PCIe-inclusive rate a host caller gets (never `value`): the same
+    batch through the host-buffer C ABI dpf_evalfull_batch (keys H2D, output
+    D2H into caller memory, synchronous; dpf.go:243-262's EvalFull returns a
+    fresh slice).  Two destinations: a FRESH array per call (first touch of
+    its pages inside the call; the caller's later free is its own and is
+    timed apart) and a REUSED array.  Median of `reps` calls."""
+    dpf = c.dpf
+    nk = ka.shape[0]
+    shape = (nk, dpf.evalfull_len(logN))
+    out_b = shape[0] * shape[1]
+    reuse = np.empty(shape, np.uint8)
+    dpf.evalfull_batch(ka, logN, ngpus=1, out=reuse)
+    t_reuse, t_fresh, t_free = [], [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dpf.evalfull_batch(ka, logN, ngpus=1, out=reuse)
+        t_reuse.append(time.perf_counter() - t0)
+    for _ in range(reps):
+        out = np.empty(shape, np.uint8)
+        t0 = time.perf_counter()
+        dpf.evalfull_batch(ka, logN, ngpus=1, out=out)
+        t1 = time.perf_counter()
+        del out
+        t_free.append(time.perf_counter() - t1)
+        t_fresh.append(t1 - t0)
+    med = lambda v: float(np.median(v))  # noqa: E731
+    return {"entry": "dpf_evalfull_batch (host buffers, synchronous)", "bytes_out": out_b,
+            "reused_out": {"ms": round(med(t_reuse) * 1e3, 3), "points_per_s": nk * (1 << logN) / med(t_reuse),
+                           "D2H_GBs": round(out_b / med(t_reuse) / 1e9, 2)},
+            "fresh_out": {"ms": round(med(t_fresh) * 1e3, 3), "points_per_s": nk * (1 << logN) / med(t_fresh),
+                          "D2H_GBs": round(out_b / med(t_fresh) / 1e9, 2),
+                          "caller_free_ms": round(med(t_free) * 1e3, 3)}}
 
 
 def wl_eval(c: Ctx) -> dict:
@@ -346,16 +383,19 @@ def wl_eval(c: Ctx) -> dict:
         assert np.array_equal(got, oracle.eval_batch(ka[:64], xs[:64], logN, nthreads=8)), "Eval differs"
     sec = t_wall / a.steps
     q = nk * ppk
-    aes = q * (stop_of(logN) + 1)
+    aes = q * (stop_of(logN) + 1)                    # algorithmic per-query walks (SURVEY §8a A_eval)
+    L = dpf.eval_frontier_level(logN, ppk)
+    aes_done = nk * ((1 << (L + 1)) - 2 if L else 0) + q * (stop_of(logN) - L + 1)   # what the kernels compute
     line = c.line(metric="DPF Eval point queries/sec (batched Eval)", value=q * c.world / sec, unit="queries/s",
                   ms_per_step=sec * 1e3, scaling="weak", data="synthetic keys + uniform points",
                   config={"workload": f"batched Eval, {nk} keys x {ppk} points, logN={logN} per GPU "
                                       f"(BASELINE configs[2])", "logN": logN, "parallelism": f"key-shard x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+[k_evalfull<nodes>]+k_eval", k_ms,
+    line["roofline"] = prg_roofline(aes_done / (k_ms * 1e-3), "k_unpack+[k_evalfull<nodes>]+k_eval", k_ms,
                                     q * 9 + nk * (stop_of(logN) + 2) * 32)
-    line["roofline"]["note"] = ("aes_blocks_per_s counts the reference-shaped stop+1 AES per query; the shared "
-                                "frontier computes fewer, so frac can exceed the kernel's true VALU share")
+    line["roofline"]["note"] = (f"achieved counts the AES the kernels compute: a shared frontier at level {L} "
+                                f"(2^(L+1)-2 per key) + stop-L+1 per query = {aes_done / q:.2f} per query, against "
+                                f"the per-query walk's {stop_of(logN) + 1} (aes_blocks_per_s above)")
     return line
 
 
@@ -516,6 +556,7 @@ def main() -> None:
     ap.add_argument("--aes", choices=["ttable", "bitsliced"], default=None,
                     help="tree-kernel AES back end for the headline (default: the library's)")
     ap.add_argument("--no-variants", action="store_true", help="skip timing the other AES back end")
+    ap.add_argument("--no-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) API rates")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--check", action="store_true", help="verify a sample of outputs against the oracle")
     ap.add_argument("--dry-run", action="store_true",

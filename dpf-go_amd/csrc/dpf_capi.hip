@@ -6,8 +6,12 @@
 // There is no CPU evaluation path: without a usable gfx950 device every
 // evaluation call fails with DPF_ERR_NODEV.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -104,13 +108,51 @@ class CopyPool {
         static CopyPool pool;
         return pool;
     }
+    // memcpy over the pool in 2 MiB pieces.
     void memcpy_par(void* dst, const void* src, size_t n) {
-        constexpr size_t kPiece = (size_t)2 << 20;
         if (n <= kPiece || workers_.empty()) {
             memcpy(dst, src, n);
             return;
         }
-        Job job{static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n, (n + kPiece - 1) / kPiece};
+        struct Ctx {
+            uint8_t* d;
+            const uint8_t* s;
+            size_t n;
+        } c{static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n};
+        parallel_for((n + kPiece - 1) / kPiece, &c, [](void* p, size_t i) {
+            const Ctx& x = *static_cast<const Ctx*>(p);
+            const size_t off = i * kPiece;
+            memcpy(x.d + off, x.s + off, std::min(kPiece, x.n - off));
+        });
+    }
+    // First touch of a (fresh) destination, one write per 4 KiB page, so the
+    // page faults -- one per 2 MiB with transparent huge pages -- are taken
+    // by all workers at once instead of inside the timed copies.
+    void prefault_par(void* dst, size_t n) {
+        struct Ctx {
+            volatile uint8_t* d;
+            size_t n;
+        } c{static_cast<volatile uint8_t*>(dst), n};
+        parallel_for((n + kPiece - 1) / kPiece, &c, [](void* p, size_t i) {
+            const Ctx& x = *static_cast<const Ctx*>(p);
+            const size_t off = i * kPiece, end = std::min(off + kPiece, x.n);
+            for (size_t o = off; o < end; o += 4096) x.d[o] = 0;
+        });
+    }
+
+   private:
+    static constexpr size_t kPiece = (size_t)2 << 20;
+    struct Job {
+        void (*fn)(void*, size_t);
+        void* ctx;
+        size_t npieces;
+        size_t active = 0;   // workers inside run(); guarded by mu_
+        std::atomic<size_t> next{0}, done{0};
+        Job(void (*f)(void*, size_t), void* c, size_t np) : fn(f), ctx(c), npieces(np) {}
+    };
+    // fn(ctx, i) for i < npieces over the caller and the workers.
+    void parallel_for(size_t npieces, void* ctx, void (*fn)(void*, size_t)) {
+        Job job{fn, ctx, npieces};
         {
             std::lock_guard<std::mutex> lk(mu_);
             jobs_.push_back(&job);
@@ -122,29 +164,35 @@ class CopyPool {
         done_cv_.wait(lk, [&] { return job.done.load() == job.npieces && job.active == 0; });
         jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));
     }
-
-   private:
-    struct Job {
-        uint8_t* dst;
-        const uint8_t* src;
-        size_t n, npieces;
-        size_t active = 0;   // workers inside run(); guarded by mu_
-        std::atomic<size_t> next{0}, done{0};
-        Job(uint8_t* d, const uint8_t* s, size_t nn, size_t np) : dst(d), src(s), n(nn), npieces(np) {}
-    };
-    // Copy pieces of `job` until none is left.
+    // Run pieces of `job` until none is left.
     static void run(Job& job) {
-        constexpr size_t kPiece = (size_t)2 << 20;
         for (size_t i; (i = job.next.fetch_add(1)) < job.npieces;) {
-            const size_t off = i * kPiece, len = std::min(kPiece, job.n - off);
-            memcpy(job.dst + off, job.src + off, len);
+            job.fn(job.ctx, i);
             job.done.fetch_add(1);
         }
     }
+    // One worker per CPU this process may use (affinity mask, capped by a
+    // cgroup CPU quota), minus the caller, at most 31: first-touch page
+    // faults of a fresh caller buffer and the copy itself both scale with
+    // threads (one thread copies ~10 GB/s; PCIe delivers ~50).
     CopyPool() {
-        unsigned hw = std::thread::hardware_concurrency();
-        const unsigned n = std::min(7u, hw > 1 ? hw - 1 : 0u);
+        const unsigned n = std::min(31u, usable_cpus() > 1 ? usable_cpus() - 1 : 0u);
         for (unsigned i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    static unsigned usable_cpus() {
+        unsigned n = std::thread::hardware_concurrency();
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof set, &set) == 0) n = (unsigned)CPU_COUNT(&set);
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            unsigned long per = 0;
+            if (fscanf(f, "%31s %lu", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+                const unsigned long quota = strtoul(q, nullptr, 10) / per;
+                if (quota >= 1 && quota < n) n = (unsigned)quota;
+            }
+            fclose(f);
+        }
+        return n > 0 ? n : 1;
     }
     ~CopyPool() {
         {
@@ -358,15 +406,28 @@ int ensure_staging(Dev& d, size_t chunk_cap) {
     return DPF_OK;
 }
 
+// Large caller buffers (a fresh Go slice / numpy array): ask for
+// transparent huge pages, so first touch costs one fault per 2 MiB instead
+// of per 4 KiB (a no-op where THP is off or the pages already exist).
+void hint_hugepages(uint8_t* p, size_t n) {
+    if (n < ((size_t)64 << 20)) return;
+    const uintptr_t a = ((uintptr_t)p + ((1u << 21) - 1)) & ~(uintptr_t)((1u << 21) - 1);
+    const uintptr_t e = ((uintptr_t)p + n) & ~(uintptr_t)((1u << 21) - 1);
+    if (e > a) (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
+}
+
 template <class Produce>
-int pipeline_d2h(Dev& d, size_t nchunks, size_t chunk_cap, Produce produce, uint8_t* out) {
+int pipeline_d2h(Dev& d, size_t nchunks, size_t chunk_cap, Produce produce, uint8_t* out, size_t out_bytes,
+                 size_t out_base = 0) {
+    // Chunk i lands at out + off_i - out_base; [out, out + out_bytes) is the whole destination.
     if (nchunks == 0) return DPF_OK;
+    hint_hugepages(out, out_bytes);
     if (int rc = ensure_staging(d, chunk_cap)) return rc;
     size_t bytes[2] = {0, 0}, off[2] = {0, 0};
     auto drain = [&](size_t i) -> int {              // chunk i: wait for its PCIe copy, then host copy
         const int s = (int)(i & 1);
         HIP_TRY(hipEventSynchronize(d.ev_c[s]));
-        CopyPool::get().memcpy_par(out + off[s], d.pin[s].p, bytes[s]);
+        CopyPool::get().memcpy_par(out + (off[s] - out_base), d.pin[s].p, bytes[s]);
         return DPF_OK;
     };
     for (size_t i = 0; i < nchunks; ++i) {
@@ -378,6 +439,8 @@ int pipeline_d2h(Dev& d, size_t nchunks, size_t chunk_cap, Produce produce, uint
         HIP_TRY(hipStreamWaitEvent(d.cst, d.ev_k[s], 0));
         HIP_TRY(hipMemcpyAsync(d.pin[s].p, dbuf, bytes[s], hipMemcpyDeviceToHost, d.cst));
         HIP_TRY(hipEventRecord(d.ev_c[s], d.cst));
+        if (i == std::min<size_t>(1, nchunks - 1) && out_bytes >= ((size_t)64 << 20))
+            CopyPool::get().prefault_par(out, out_bytes);   // while the GPU works on chunks 0-1
         if (i >= 1)
             if (int rc = drain(i - 1)) return rc;          // frees pinned slot (i-1)&1 for chunk i+1
     }
@@ -405,7 +468,7 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
             bytes = n * olen;
             off = k0 * olen;
             return DPF_OK;
-        }, out);
+        }, out, nk * olen);
     }
     uint32_t pb = 0;                                      // one key's output exceeds a chunk: subtree slabs
     while ((olen >> pb) > kStageBytes) ++pb;
@@ -416,7 +479,7 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
         bytes = slab;
         off = k * olen + p * slab;
         return DPF_OK;
-    }, out);
+    }, out, nk * olen);
 }
 
 size_t pir_ek_bytes(size_t nkeys, uint32_t logN);
@@ -661,7 +724,7 @@ int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* 
             bytes = sub;
             off = lo * slab + j * sub;
             return DPF_OK;
-        }, out);
+        }, out + lo * slab, slab, lo * slab);
     });
 }
 
@@ -687,6 +750,10 @@ int dpf_evalfull_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_
 
 size_t dpf_eval_workspace_size(size_t nkeys, size_t pts_per_key, uint32_t logN) {
     return std::max<size_t>(16, eval_work_bytes(nkeys, pts_per_key, logN));
+}
+
+uint32_t dpf_eval_frontier_level(uint32_t logN, size_t pts_per_key) {
+    return dpfk::eval_frontier_level(stop_of(logN), pts_per_key);
 }
 
 int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, const uint64_t* d_xs,

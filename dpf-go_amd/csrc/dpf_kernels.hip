@@ -425,8 +425,9 @@ hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, ui
 }
 
 uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key) {
-    // Shared frontier at level L when a key's points cover it twice over:
-    // 2^(L+2) <= ppk, i.e. >= 4 points per frontier node (and L >= 4).
+    // Shared frontier at the deepest level L whose nodes a key's points cover
+    // twice over on average: 2^(L+1) <= ppk, i.e. >= 2 points per frontier
+    // node (L = 9 at 1024 points per key), used when L >= 4.
     uint32_t L = 0;
     while (L < kMaxFrontierHbm && L < stop && (2ull << (L + 1)) <= pts_per_key) ++L;
     return L >= 4 ? L : 0;

@@ -73,6 +73,7 @@ SIGNATURES = {
     "dpf_evalfull_batch_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp, _vp]),
     "dpf_evalfull_subtree_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _vp, _vp]),
     "dpf_eval_workspace_size": (_sz, [_sz, _sz, _u32]),
+    "dpf_eval_frontier_level": (_u32, [_u32, _sz]),
     "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _sz, _vp]),
     "dpf_expand_keys_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp]),
     "dpf_evalfull_expanded_dev": (_int, [_int, _vp, _sz, _u32, _u32, _u64, _vp, _vp]),
@@ -275,6 +276,11 @@ def evalfull_subtree_dev(d_keys, key_len_: int, nkeys: int, logN: int, prefix_bi
 
 def eval_workspace_size(nkeys: int, pts_per_key: int, logN: int) -> int:
     return int(lib().dpf_eval_workspace_size(nkeys, pts_per_key, logN))
+
+
+def eval_frontier_level(logN: int, pts_per_key: int) -> int:
+    """Depth of the shared frontier eval_batch_dev uses with a full workspace (0: root walks)."""
+    return int(lib().dpf_eval_frontier_level(logN, pts_per_key))
 
 
 def eval_batch_dev(d_keys, key_len_: int, nkeys: int, d_xs, pts_per_key: int, logN: int, d_out, d_work,

@@ -111,6 +111,10 @@ int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t key_len, 
  * once); with only dpf_workspace_size(nkeys, logN) bytes each query walks
  * from the root.  Results are identical either way. */
 size_t dpf_eval_workspace_size(size_t nkeys, size_t pts_per_key, uint32_t logN);
+/* Depth L of that shared frontier (0: none).  Work with the frontier:
+ * 2^(L+1)-2 AES per key for the frontier nodes, then logN-7-L+1 per query
+ * (against the reference's 2*(logN-7)+1, dpf.go:183-209). */
+uint32_t dpf_eval_frontier_level(uint32_t logN, size_t pts_per_key);
 int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, const uint64_t* d_xs,
                        size_t pts_per_key, uint32_t logN, uint8_t* d_out, void* d_work, size_t work_bytes,
                        void* stream);
