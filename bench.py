@@ -229,6 +229,17 @@ class Ctx:
         max-over-ranks wall time and the mean kernel time of the event pairs."""
         torch, dist = self.torch, self.dist
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        # Clock spin-up (untimed, before the W warmup steps): an idle MI355X
+        # needs a few hundred ms of load to reach its steady-state clock; a
+        # 5-step warmup (~6 ms) left configs[1] at 1.174 ms/launch against
+        # 1.069 ms after 60 steps (profiles/r02/warmup).  Steady state is what
+        # a busy server sees, so every workload first runs its own step for
+        # SPINUP_S seconds of wall time.
+        t_spin = time.perf_counter()
+        while time.perf_counter() - t_spin < self.args.spinup:
+            for _ in range(4):
+                step(None)
+            torch.cuda.synchronize(self.dev)
         for _ in range(warmup):
             step(None)
         torch.cuda.synchronize(self.dev)
@@ -252,6 +263,7 @@ class Ctx:
 
     def line(self, **kw):
         base = {"n_gpus": self.world, "steps": self.args.steps, "warmup": self.args.warmup,
+                "spinup_s": self.args.spinup,
                 "higher_is_better": True, "vs_baseline": None, "dtype": "u32"}
         base.update(kw)
         return base
@@ -558,6 +570,8 @@ def main() -> None:
     ap.add_argument("--no-variants", action="store_true", help="skip timing the other AES back end")
     ap.add_argument("--no-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) API rates")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--spinup", type=float, default=0.5,
+                    help="seconds of untimed steps before the warmup (GPU clock ramp); 0 disables")
     ap.add_argument("--check", action="store_true", help="verify a sample of outputs against the oracle")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/collective plumbing only (gloo, no GPU): what the CPU tests run")

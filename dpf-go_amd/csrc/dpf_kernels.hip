@@ -124,6 +124,26 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
             store16(c.outp, leaf_fix(o, n.t, c.fcw));
             c.outp += 16;
         }
+    } else if constexpr (D == 2 && !NODES) {
+        // Bottom two levels at once: 4 leaves = 64 contiguous bytes stored back
+        // to back.  Pairs of 32-B stores three AES apart left partial lines to
+        // be written twice: WRITE_SIZE 1.47x -> 1.28x the 512 MiB output, 1%
+        // faster (profiles/r02/variants).
+        CW cw = load_cw(c.ek, lvl0 + DMAX - 2);
+        Node L, R;
+        expand(c.tab, c.lo, n, cw, L, R);
+        CW cw1 = load_cw(c.ek, lvl0 + DMAX - 1);
+        Node LL, LR, RL, RR;
+        expand(c.tab, c.lo, L, cw1, LL, LR);
+        expand(c.tab, c.lo, R, cw1, RL, RR);
+        Blk o0, o1, o2, o3;
+        mmo_pair(c.tab, c.lo, KeyFixed<false>{}, LL.s, o0, KeyFixed<false>{}, LR.s, o1);
+        mmo_pair(c.tab, c.lo, KeyFixed<false>{}, RL.s, o2, KeyFixed<false>{}, RR.s, o3);
+        store16(c.outp, leaf_fix(o0, LL.t, c.fcw));
+        store16(c.outp + 16, leaf_fix(o1, LR.t, c.fcw));
+        store16(c.outp + 32, leaf_fix(o2, RL.t, c.fcw));
+        store16(c.outp + 48, leaf_fix(o3, RR.t, c.fcw));
+        c.outp += 64;
     } else if constexpr (D == 1) {
         CW cw = load_cw(c.ek, lvl0 + DMAX - 1);
         Node L, R;

@@ -1,0 +1,18 @@
+#!/bin/bash
+# End-of-milestone GPU pass: parity tests + the 4 bench lines (tools/gpu_round.sh),
+# the default bench under rocprofv3 kernel-trace + PMC passes (tools/profile.sh),
+# kernel traces of the secondary workloads, and the Go toolchain probe.
+#   tools/round_profile.sh <tag>     -> gpurun_out/<tag>/...
+set -uo pipefail
+REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$REPO"
+T="${1:-round}"
+bash tools/gpu_round.sh "$T" || exit $?
+bash tools/profile.sh "gpurun_out/$T/prof" > "gpurun_out/$T/profile.log" 2>&1 || { tail -20 "gpurun_out/$T/profile.log"; exit 1; }
+export TMPDIR=/tmp
+for w in eval split pir; do
+  ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$REPO/gpurun_out/$T/kt_$w" -o kt --output-format csv -- \
+      python3 "$REPO/bench.py" --workload $w --steps 20 --warmup 5 > "$REPO/gpurun_out/$T/kt_$w.log" 2>&1 ) || { echo "kt $w failed"; exit 1; }
+done
+{ command -v go && go version; } > "gpurun_out/$T/go_probe.txt" 2>&1 || echo "go: not found on the GPU box ($(date -u +%FT%TZ))" > "gpurun_out/$T/go_probe.txt"
+echo "round profile done"
