@@ -660,6 +660,18 @@ int dpf_gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s
     return rc ? fail(rc, "dpf: invalid parameters") : DPF_OK;
 }
 
+int dpf_keys_pack(const uint8_t* const* keys, const size_t* lens, size_t n, size_t key_len, uint8_t* out) {
+    int rc = dpfh::keys_pack(keys, lens, n, key_len, out);
+    return rc == DPF_ERR_KEYLEN ? fail(rc, "dpf: key length differs from the batch's key_len")
+           : rc                ? fail(rc, "dpf: invalid parameters")
+                               : DPF_OK;
+}
+
+int dpf_keys_unpack(const uint8_t* packed, size_t key_len, size_t n, uint8_t* const* keys) {
+    int rc = dpfh::keys_unpack(packed, key_len, n, keys);
+    return rc ? fail(rc, "dpf: invalid parameters") : DPF_OK;
+}
+
 int dpf_evalfull_batch(const uint8_t* keys, size_t klen, size_t nkeys, uint32_t logN, uint8_t* out, int ngpus) {
     if (int rc = check_key(klen, logN)) return rc;
     if (nkeys == 0) return DPF_OK;

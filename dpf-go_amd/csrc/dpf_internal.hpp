@@ -14,5 +14,7 @@ int gen_seeded(uint64_t alpha, uint32_t logN, const uint8_t s0[16], const uint8_
 int gen_random(uint64_t alpha, uint32_t logN, uint8_t* ka, uint8_t* kb);
 int gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, const uint8_t* s1s, size_t n,
                      uint8_t* kas, uint8_t* kbs, int nthreads);
+int keys_pack(const uint8_t* const* keys, const size_t* lens, size_t n, size_t key_len, uint8_t* out);
+int keys_unpack(const uint8_t* packed, size_t key_len, size_t n, uint8_t* const* keys);
 
 }  // namespace dpfh

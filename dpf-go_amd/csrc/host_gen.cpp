@@ -10,6 +10,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <functional>
 #include <stdexcept>
 #include <thread>
 #include <vector>
@@ -362,6 +363,45 @@ int gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, 
     for (int i = 1; i < nt; ++i) th.emplace_back(work, i);
     work(0);
     for (auto& x : th) x.join();
+    return DPF_OK;
+}
+
+// Key wire format.  A key is the reference's DPFkey bytes
+// (dpf.go:7,89-92,111-112,137-138,165-167) and a batch is [n][key_len]
+// contiguous, which is what Gen writes and every evaluation entry reads; so
+// (de)serialising a batch is a gather / scatter of whole keys.  Large batches
+// are copied on several threads (one 64-key block per task at least).
+static void copy_keys(size_t n, size_t kl, const std::function<void(size_t)>& one) {
+    const size_t bytes = n * kl;
+    int nt = bytes < ((size_t)8 << 20) ? 1 : std::min(16, usable_cpus());
+    nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(n / 64, 1));
+    auto work = [&](int tid) {
+        const size_t lo = n * (size_t)tid / (size_t)nt, hi = n * (size_t)(tid + 1) / (size_t)nt;
+        for (size_t i = lo; i < hi; ++i) one(i);
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt; ++i) th.emplace_back(work, i);
+    work(0);
+    for (auto& x : th) x.join();
+}
+
+int keys_pack(const uint8_t* const* keys, const size_t* lens, size_t n, size_t key_len, uint8_t* out) {
+    if (n == 0) return DPF_OK;
+    if (!keys || !out || key_len == 0) return DPF_ERR_PARAM;
+    for (size_t i = 0; i < n; ++i) {
+        if (!keys[i]) return DPF_ERR_PARAM;
+        if (lens && lens[i] != key_len) return DPF_ERR_KEYLEN;
+    }
+    copy_keys(n, key_len, [&](size_t i) { memcpy(out + i * key_len, keys[i], key_len); });
+    return DPF_OK;
+}
+
+int keys_unpack(const uint8_t* packed, size_t key_len, size_t n, uint8_t* const* keys) {
+    if (n == 0) return DPF_OK;
+    if (!keys || !packed || key_len == 0) return DPF_ERR_PARAM;
+    for (size_t i = 0; i < n; ++i)
+        if (!keys[i]) return DPF_ERR_PARAM;
+    copy_keys(n, key_len, [&](size_t i) { memcpy(keys[i], packed + i * key_len, key_len); });
     return DPF_OK;
 }
 

@@ -65,6 +65,8 @@ SIGNATURES = {
     "dpf_gen_seeded": (_int, [_u64, _u32, _u8p, _u8p, _u8p, _u8p]),
     "dpf_gen": (_int, [_u64, _u32, _u8p, _u8p]),
     "dpf_gen_batch_seeded": (_int, [_u64p, _u32, _u8p, _u8p, _sz, _u8p, _u8p, _int]),
+    "dpf_keys_pack": (_int, [ctypes.POINTER(_vp), ctypes.POINTER(_sz), _sz, _sz, _u8p]),
+    "dpf_keys_unpack": (_int, [_u8p, _sz, _sz, ctypes.POINTER(_vp)]),
     "dpf_eval": (_int, [_u8p, _sz, _u64, _u32, _u8p]),
     "dpf_evalfull": (_int, [_u8p, _sz, _u32, _u8p]),
     "dpf_evalfull_batch": (_int, [_u8p, _sz, _sz, _u32, _u8p, _int]),
@@ -159,6 +161,34 @@ def gpu_init_devices(ordinals: Sequence[int]) -> int:
 
 def gpu_shutdown() -> None:
     lib().dpf_gpu_shutdown()
+
+
+# ------------------------------------------------------- key wire format ---
+def keys_pack(keys: Sequence[bytes], key_len: Optional[int] = None) -> np.ndarray:
+    """[DPFkey, ...] -> uint8[n, key_len], the batch layout of every batched
+    entry point (dpf_keys_pack).  Keys are the reference's bytes (dpf.go:7);
+    all must have the same length (DPFPanic DPF_ERR_KEYLEN otherwise)."""
+    bufs = [_as_u8(k) for k in keys]
+    n = len(bufs)
+    kl = key_len if key_len is not None else (bufs[0].size if n else 0)
+    out = np.empty((n, kl), np.uint8)
+    if n == 0:
+        return out
+    ptrs = (_vp * n)(*[b.ctypes.data for b in bufs])
+    lens = (_sz * n)(*[b.size for b in bufs])
+    _check(lib().dpf_keys_pack(ptrs, lens, n, kl, _buf(out)))
+    return out
+
+
+def keys_unpack(packed: np.ndarray) -> list:
+    """uint8[n, key_len] -> [DPFkey (bytes), ...] (dpf_keys_unpack)."""
+    a = np.ascontiguousarray(packed, dtype=np.uint8)
+    n, kl = a.shape
+    outs = [np.empty(kl, np.uint8) for _ in range(n)]
+    if n:
+        ptrs = (_vp * n)(*[o.ctypes.data for o in outs])
+        _check(lib().dpf_keys_unpack(_buf(a), kl, n, ptrs))
+    return [o.tobytes() for o in outs]
 
 
 # ------------------------------------------------------------------ Gen ---

@@ -76,6 +76,18 @@ int dpf_gen(uint64_t alpha, uint32_t logN, uint8_t* ka, uint8_t* kb);
 int dpf_gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, const uint8_t* s1s, size_t n,
                          uint8_t* kas, uint8_t* kbs, int nthreads);
 
+/* ---- key wire format ------------------------------------ */
+/* A key is the reference's DPFkey bytes (type DPFkey []byte, dpf.go:7; layout
+ * dpf.go:89-92,111-112,137-138,165-167), so a key made by the Go Gen is a
+ * valid input here and vice versa.  A batch is [n][key_len] contiguous (what
+ * dpf_gen_batch_seeded writes and every batched entry reads).
+ * dpf_keys_pack gathers n keys (pointers; lens[i] must equal key_len, or
+ * lens = NULL) into out[n][key_len]: DPF_ERR_KEYLEN on a length mismatch.
+ * dpf_keys_unpack scatters a batch back to n key buffers of key_len bytes.
+ * Host-only; large batches are copied on several threads. */
+int dpf_keys_pack(const uint8_t* const* keys, const size_t* lens, size_t n, size_t key_len, uint8_t* out);
+int dpf_keys_unpack(const uint8_t* packed, size_t key_len, size_t n, uint8_t* const* keys);
+
 /* ---- evaluation, host buffers (synchronous; PCIe-inclusive) ------------ */
 /* Keys: at least 17 + 18*stop bytes (the reference's own index bound,
  * dpf.go:175-176,186-188); the final CW is always k[len-16 : len]

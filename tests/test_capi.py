@@ -53,6 +53,29 @@ def test_host_gen_matches_golden():
         assert ka.hex() == c["ka"] and kb.hex() == c["kb"]
 
 
+def test_key_pack_unpack_roundtrip():
+    """Key wire format: a batch is [n][key_len] of the
+    reference's DPFkey bytes; pack/unpack are exact inverses, also on the
+    multi-threaded path (> 8 MiB)."""
+    for logN, n in ((20, 1), (20, 300), (3, 5), (24, 30000)):
+        al, s0, s1 = synth.key_seeds(n, logN)
+        ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+        keys = [bytes(k) for k in ka]
+        packed = dpf.keys_pack(keys)
+        assert packed.shape == (n, dpf.key_len(logN)) and np.array_equal(packed, ka)
+        assert dpf.keys_unpack(packed) == keys
+    assert dpf.keys_pack([]).shape == (0, 0)
+
+
+def test_key_pack_rejects_ragged_batches():
+    ka, kb = dpf.gen_seeded(5, 9, bytes(16), bytes(range(16)))
+    with pytest.raises(dpf.DPFPanic) as e:
+        dpf.keys_pack([ka, kb[:-1]])
+    assert e.value.code == dpf.DPF_ERR_KEYLEN
+    with pytest.raises(dpf.DPFPanic):
+        dpf.keys_pack([ka], key_len=len(ka) + 1)
+
+
 def test_batch_gen_matches_single():
     logN = 20
     al, s0, s1 = synth.key_seeds(64, logN)
