@@ -833,8 +833,28 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st));
     HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st));
     uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
-    HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, (uint32_t)nkeys, (uint32_t*)d_ans, parts,
-                                  st));
+    HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, 32, (uint32_t)nkeys, (uint32_t*)d_ans,
+                                  parts, st));
+    return DPF_OK;
+}
+
+size_t dpf_xor_fold_workspace_size(void) { return dpfk::pir_fold_parts_bytes(); }
+
+int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_payload,
+                     uint64_t nrec, size_t rec_bytes, uint8_t* d_ans, void* d_work, void* stream) {
+    if (rec_bytes == 0 || rec_bytes % 32 != 0) return fail(DPF_ERR_PARAM, "dpf: rec_bytes must be a positive multiple of 32");
+    if (bits_stride % 16 != 0) return fail(DPF_ERR_PARAM, "dpf: bits_stride must be a multiple of 16");
+    if (nrec > (uint64_t)bits_stride * 8) return fail(DPF_ERR_PARAM, "dpf: more records than selection bits per key");
+    if (((uintptr_t)d_bits | (uintptr_t)d_payload) % 16 != 0 || (uintptr_t)d_ans % 4 != 0)
+        return fail(DPF_ERR_PARAM, "dpf: misaligned device buffer");
+    if (nkeys > 0 && (!d_ans || !d_work || (nrec > 0 && (!d_bits || !d_payload))))
+        return fail(DPF_ERR_PARAM, "dpf: null device buffer");
+    DeviceGuard g(device);
+    hipStream_t st = (hipStream_t)stream;
+    if (nkeys == 0) return DPF_OK;
+    HIP_TRY(hipMemsetAsync(d_ans, 0, nkeys * rec_bytes, st));
+    HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)d_bits, bits_stride / 4, d_payload, nrec, rec_bytes, (uint32_t)nkeys,
+                                  (uint32_t*)d_ans, (uint32_t*)d_work, st));
     return DPF_OK;
 }
 

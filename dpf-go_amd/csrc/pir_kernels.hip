@@ -60,9 +60,13 @@ __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// Records may be any multiple of 32 B (rec_u4 16-byte words each); a launch
+// folds one 32-byte column `col` of every record (the PIR case: rec_u4 = 2,
+// col = 0).
 __global__ __launch_bounds__(64 * kM4Waves, 4) void k_pir_fold4r(const uint32_t* __restrict__ bits, uint64_t wpk,
                                                               const uint4* __restrict__ db, uint64_t nrec,
-                                                              uint32_t nkeys, uint64_t chunks_per_block,
+                                                              uint64_t rec_u4, uint32_t col, uint32_t nkeys,
+                                                              uint64_t chunks_per_block,
                                                               uint32_t* __restrict__ parts) {
     __shared__ uint4 s_tab[kM4Waves][kM4Groups * 2 * 16];
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[kM4MaxKeys * kSelRow];
@@ -94,8 +98,8 @@ __global__ __launch_bounds__(64 * kM4Waves, 4) void k_pir_fold4r(const uint32_t*
         uint64_t ra = cc * 64 + (l >> 1), rb = ra + 32;
         if (ra >= nrec) ra = nrec - 1;
         if (rb >= nrec) rb = nrec - 1;
-        A = db[2 * ra + (l & 1)];
-        B = db[2 * rb + (l & 1)];
+        A = db[rec_u4 * ra + 2 * col + (l & 1)];
+        B = db[rec_u4 * rb + 2 * col + (l & 1)];
     };
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -178,15 +182,16 @@ __global__ __launch_bounds__(64 * kM4Waves, 4) void k_pir_fold4r(const uint32_t*
     }
 }
 
-// ans[k][i] ^= XOR over workgroups of parts[wg][k][i] (k < nkeys).  Block
-// (x, y): 256 answer words x parts y, y + gridDim.y, ...; one atomicXor each.
+// ans[k * ans_words + i] ^= XOR over workgroups of parts[wg][k][i] (k <
+// nkeys, i < 8).  Block (x, y): 256 answer words x parts y, y + gridDim.y,
+// ...; one atomicXor each.
 __global__ __launch_bounds__(256) void k_xor_parts(const uint32_t* __restrict__ parts, uint64_t nparts,
-                                                   uint32_t nkeys, uint32_t* __restrict__ ans) {
+                                                   uint32_t nkeys, uint32_t* __restrict__ ans, uint64_t ans_words) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;   // word index k * 8 + i
     if (t >= nkeys * 8) return;
     uint32_t v = 0;
     for (uint64_t p = blockIdx.y; p < nparts; p += gridDim.y) v ^= parts[p * kM4MaxKeys * 8 + t];
-    if (v) atomicXor(ans + t, v);
+    if (v) atomicXor(ans + (t >> 3) * ans_words + (t & 7), v);
 }
 
 static int cu_count_fold() {
@@ -202,8 +207,9 @@ constexpr uint64_t kFoldMaxBlocks = 2048;   // partials area: max fold workgroup
 uint64_t pir_fold_parts_bytes() { return kFoldMaxBlocks * kM4MaxKeys * 32; }
 
 hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const uint8_t* db, uint64_t nrec,
-                           uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
+                           uint64_t rec_bytes, uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
     if (nrec == 0 || nkeys == 0) return hipSuccess;
+    if (rec_bytes == 0 || rec_bytes % 32 != 0) return hipErrorInvalidValue;
     const uint64_t nchunks = (nrec + 63) / 64;
     // Two resident workgroups (16 waves) per CU, each over a contiguous chunk range.
     uint64_t blocks = (uint64_t)cu_count_fold() * 2;
@@ -212,14 +218,16 @@ hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const u
     cpb = (cpb + 2 * kM4Waves - 1) / (2 * kM4Waves) * (2 * kM4Waves);   // whole 16-chunk batches
     blocks = (nchunks + cpb - 1) / cpb;
     const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
-    for (uint32_t k0 = 0; k0 < nkeys; k0 += kM4MaxKeys) {
-        const uint32_t nk = nkeys - k0 < (uint32_t)kM4MaxKeys ? nkeys - k0 : (uint32_t)kM4MaxKeys;
-        hipLaunchKernelGGL(k_pir_fold4r, dim3((uint32_t)blocks), dim3(64 * kM4Waves), 0, st,
-                           bits + (uint64_t)k0 * words_per_key, words_per_key, reinterpret_cast<const uint4*>(db),
-                           nrec, nk, cpb, parts);
-        hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk,
-                           ans + (uint64_t)k0 * 8);
-    }
+    const uint64_t rec_u4 = rec_bytes / 16, ans_words = rec_bytes / 4;
+    for (uint32_t col = 0; col < rec_bytes / 32; ++col)
+        for (uint32_t k0 = 0; k0 < nkeys; k0 += kM4MaxKeys) {
+            const uint32_t nk = nkeys - k0 < (uint32_t)kM4MaxKeys ? nkeys - k0 : (uint32_t)kM4MaxKeys;
+            hipLaunchKernelGGL(k_pir_fold4r, dim3((uint32_t)blocks), dim3(64 * kM4Waves), 0, st,
+                               bits + (uint64_t)k0 * words_per_key, words_per_key, reinterpret_cast<const uint4*>(db),
+                               nrec, rec_u4, col, nk, cpb, parts);
+            hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk,
+                               ans + (uint64_t)k0 * ans_words + 8 * col, ans_words);
+        }
     return hipGetLastError();
 }
 

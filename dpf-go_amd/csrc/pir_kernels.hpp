@@ -5,11 +5,12 @@
 
 namespace dpfk {
 
-// ans[k][0..7] ^= XOR of the 32-byte records db[i] (i < nrec) whose bit i is
-// set in bits[k * words_per_key ...].  `parts` is scratch of
-// pir_fold_parts_bytes() (per-wave partial answers).
+// ans[k][0 .. rec_bytes) ^= XOR of the records db[i] (rec_bytes each, a
+// multiple of 32; i < nrec) whose bit i is set in bits[k * words_per_key
+// ...] (EvalFull's LSB-first layout).  `parts` is scratch of
+// pir_fold_parts_bytes() (per-workgroup partial answers).
 uint64_t pir_fold_parts_bytes();
 hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const uint8_t* db, uint64_t nrec,
-                           uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st);
+                           uint64_t rec_bytes, uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st);
 
 }  // namespace dpfk

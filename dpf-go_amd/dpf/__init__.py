@@ -82,6 +82,8 @@ SIGNATURES = {
     "dpf_set_aes_impl": (_int, [_int]),
     "dpf_get_aes_impl": (_int, []),
     "dpf_aes_mmo_dev": (_int, [_int, _int, _int, _vp, _vp, _sz, _u32, _vp]),
+    "dpf_xor_fold_workspace_size": (_sz, []),
+    "dpf_xor_fold_dev": (_int, [_int, _vp, _sz, _sz, _vp, _u64, _sz, _vp, _vp, _vp]),
     "dpf_pir_workspace_size": (_sz, [_sz, _u32, _u32]),
     "dpf_pir_answer_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _u64, _vp, _vp, _vp]),
     "dpf_pir_db_create": (_int, [_u8p, _u64, _u32, _int, ctypes.POINTER(_vp)]),
@@ -351,6 +353,19 @@ def aes_mmo_dev(d_in, d_out, nblocks: int, impl: int = AES_TTABLE, right: bool =
     """aes128MMO iterated `reps` times over nblocks HBM blocks (both back ends)."""
     _check(lib().dpf_aes_mmo_dev(device, impl, 1 if right else 0, _ptr(d_in), _ptr(d_out), nblocks, reps,
                                  _stream_handle(stream)))
+
+
+# ------------------------------------------------------- streaming fold ---
+def xor_fold_workspace_size() -> int:
+    return int(lib().dpf_xor_fold_workspace_size())
+
+
+def xor_fold_dev(d_bits, bits_stride: int, nkeys: int, d_payload, nrec: int, rec_bytes: int, d_ans, d_work,
+                 device: int = 0, stream=None) -> None:
+    """ans[k] = XOR of payload records i (rec_bytes each) whose bit i is set
+    in EvalFull output k, on the device (dpf_xor_fold_dev)."""
+    _check(lib().dpf_xor_fold_dev(device, _ptr(d_bits), bits_stride, nkeys, _ptr(d_payload), nrec, rec_bytes,
+                                  _ptr(d_ans), _ptr(d_work), _stream_handle(stream)))
 
 
 # ------------------------------------------------------------------ PIR ---

@@ -171,6 +171,20 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t key_len, size_t
                        uint32_t prefix_bits, uint64_t prefix, const uint8_t* d_db, uint64_t nrec, uint8_t* d_ans,
                        void* d_work, void* stream);
 
+/* Streaming consumer of EvalFull output, the PIR fold
+ * generalised to any payload: for each key k,
+ *   ans[k] = XOR over i < nrec with bit i of bits[k] set of payload[i]
+ * (bit i = bit i%8 of byte i/8, EvalFull's layout, dpf.go:251-261), computed
+ * where the EvalFull output already lives, so it never leaves HBM.
+ * d_bits [nkeys][bits_stride] (e.g. dpf_evalfull_batch_dev's output;
+ * bits_stride a multiple of 16, nrec <= 8*bits_stride), d_payload
+ * [nrec][rec_bytes] (rec_bytes a positive multiple of 32), d_ans
+ * [nkeys][rec_bytes] (overwritten), d_work dpf_xor_fold_workspace_size()
+ * bytes; 16-byte-aligned device pointers.  Asynchronous on `stream`. */
+size_t dpf_xor_fold_workspace_size(void);
+int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_payload,
+                     uint64_t nrec, size_t rec_bytes, uint8_t* d_ans, void* d_work, void* stream);
+
 /* Host form: the DB is uploaded once, sharded by top-level subtree over
  * ngpus devices (a power of two), each GPU folds its slice and the host
  * XORs the per-GPU partial answers (RCCL has no XOR reduction). */

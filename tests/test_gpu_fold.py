@@ -1,0 +1,113 @@
+"""GPU parity of the streaming XOR-fold consumer (dpf_xor_fold_dev):
+the PIR fold generalised to payload records of any multiple of 32 bytes, over
+EvalFull outputs that stay in HBM.  Checked against the XOR inner product of
+the CPU oracle's EvalFull bits (oracle/dpf_oracle.c, dpf.go:243-262) with the
+same payload, plus the 2-server property at logN=20."""
+import numpy as np
+import pytest
+
+import dpf
+from dpf import synth
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert dpf.gpu_init(1) >= 1
+
+
+def _keys(nk, logN, first=0):
+    al, s0, s1 = synth.key_seeds(nk, logN, first=first)
+    ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+    return al, ka, kb
+
+
+def _want(full: np.ndarray, payload: np.ndarray, nrec: int) -> np.ndarray:
+    """XOR of payload rows i < nrec with bit i (LSB-first) of each EvalFull row set."""
+    bits = np.unpackbits(full, axis=1, bitorder="little")[:, :nrec].astype(bool)
+    out = np.zeros((full.shape[0], payload.shape[1]), np.uint8)
+    for k in range(full.shape[0]):
+        sel = payload[bits[k]]
+        if sel.shape[0]:
+            out[k] = np.bitwise_xor.reduce(sel, axis=0)
+    return out
+
+
+def _fold(full_dev, stride, nk, payload, nrec, rec_bytes):
+    import torch
+    dev = full_dev.device
+    d_pay = torch.from_numpy(np.ascontiguousarray(payload)).to(dev)
+    d_ans = torch.full((nk * rec_bytes,), 0xAB, dtype=torch.uint8, device=dev)   # overwritten, not accumulated
+    d_work = torch.empty(dpf.xor_fold_workspace_size(), dtype=torch.uint8, device=dev)
+    dpf.xor_fold_dev(full_dev, stride, nk, d_pay, nrec, rec_bytes, d_ans, d_work)
+    torch.cuda.synchronize()
+    return d_ans.cpu().numpy().reshape(nk, rec_bytes)
+
+
+@pytest.mark.parametrize("logN,nk,rec_bytes,nrec", [
+    (7, 3, 32, 128), (10, 5, 64, 1000), (12, 70, 96, 4096), (13, 9, 256, 5000), (14, 64, 32, 16384),
+])
+def test_xor_fold_matches_oracle(logN, nk, rec_bytes, nrec):
+    import torch
+    _, ka, _ = _keys(nk, logN, first=100 + logN)
+    full = oracle.evalfull_batch(ka, logN, nthreads=8)
+    stride = dpf.evalfull_len(logN)
+    payload = synth.db_bytes(nrec * rec_bytes).reshape(nrec, rec_bytes)
+    kl = dpf.key_len(logN)
+    d_keys = torch.from_numpy(ka.reshape(-1)).cuda()
+    d_full = torch.empty(nk * stride, dtype=torch.uint8, device="cuda")
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device="cuda")
+    dpf.evalfull_batch_dev(d_keys, kl, nk, logN, d_full, d_work)    # the output never leaves HBM
+    torch.cuda.synchronize()
+    got = _fold(d_full, stride, nk, payload, nrec, rec_bytes)
+    assert np.array_equal(got, _want(full, payload, nrec))
+
+
+def test_xor_fold_two_server_property_logN20():
+    """answer(ka) ^ answer(kb) == payload[alpha] for 128-byte records at logN=20."""
+    import torch
+    logN, nk, rec = 20, 16, 128
+    nrec = 1 << logN
+    al, ka, kb = _keys(nk, logN, first=7)
+    payload = synth.db_bytes(nrec * rec).reshape(nrec, rec)
+    stride, kl = dpf.evalfull_len(logN), dpf.key_len(logN)
+    outs = []
+    for keys in (ka, kb):
+        d_keys = torch.from_numpy(keys.reshape(-1)).cuda()
+        d_full = torch.empty(nk * stride, dtype=torch.uint8, device="cuda")
+        d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device="cuda")
+        dpf.evalfull_batch_dev(d_keys, kl, nk, logN, d_full, d_work)
+        outs.append(_fold(d_full, stride, nk, payload, nrec, rec))
+    x = outs[0] ^ outs[1]
+    for k in range(nk):
+        assert np.array_equal(x[k], payload[int(al[k])])
+
+
+def test_xor_fold_equals_pir_answer_for_32_byte_records():
+    import torch
+    logN, nk = 12, 20
+    nrec = 1 << logN
+    _, ka, _ = _keys(nk, logN, first=3)
+    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    pdb = dpf.PirDB(db, logN, ngpus=1)
+    want = pdb.answer(ka)
+    pdb.close()
+    stride, kl = dpf.evalfull_len(logN), dpf.key_len(logN)
+    d_keys = torch.from_numpy(ka.reshape(-1)).cuda()
+    d_full = torch.empty(nk * stride, dtype=torch.uint8, device="cuda")
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device="cuda")
+    dpf.evalfull_batch_dev(d_keys, kl, nk, logN, d_full, d_work)
+    assert np.array_equal(_fold(d_full, stride, nk, db, nrec, 32), want)
+
+
+def test_xor_fold_rejects_bad_shapes():
+    import torch
+    d = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    w = torch.empty(dpf.xor_fold_workspace_size(), dtype=torch.uint8, device="cuda")
+    for stride, nrec, rec in ((16, 128, 48), (24, 8, 32), (16, 129, 32)):
+        with pytest.raises(dpf.DPFPanic) as e:
+            dpf.xor_fold_dev(d, stride, 1, d, nrec, rec, d, w)
+        assert e.value.code == dpf.DPF_ERR_PARAM
+    dpf.xor_fold_dev(d, 16, 0, d, 128, 32, d, w)   # no keys: nothing to do

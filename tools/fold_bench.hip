@@ -32,11 +32,11 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int i = 0; i < 3; ++i)
-        CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, nkeys, (uint32_t*)ans,
+        CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, 32, nkeys, (uint32_t*)ans,
                                  (uint32_t*)parts, 0));
     CK(hipEventRecord(e0, 0));
     for (int i = 0; i < iters; ++i)
-        CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, nkeys, (uint32_t*)ans,
+        CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, 32, nkeys, (uint32_t*)ans,
                                  (uint32_t*)parts, 0));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
