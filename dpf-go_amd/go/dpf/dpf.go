@@ -127,3 +127,53 @@ func EvalBatch(keys []DPFkey, xs [][]uint64, logN uint64, ngpus int) [][]byte {
 	}
 	return out
 }
+
+// PirDB is one PIR server's database of 32-byte records on the GPUs
+// (dpf_pir_db_create): records are sharded over ngpus devices by top-level
+// subtree, and Answer returns this server's 32-byte share per query key:
+// the XOR of the records whose EvalFull bit is set (dpf.go:243-262).
+type PirDB struct {
+	h unsafe.Pointer
+}
+
+// NewPirDB uploads db (len(db)/32 records, at most 2^logN) to ngpus GPUs.
+func NewPirDB(db []byte, logN uint64, ngpus int) *PirDB {
+	if len(db)%32 != 0 {
+		panic("dpf: PIR records are 32 bytes")
+	}
+	p := &PirDB{}
+	var h unsafe.Pointer
+	check(C.dpf_pir_db_create(u8(db), C.uint64_t(len(db)/32), C.uint32_t(logN), C.int(ngpus), &h))
+	p.h = h
+	return p
+}
+
+// Answer returns 32 bytes per key: keys[i]'s share of DB[alpha_i].
+func (p *PirDB) Answer(keys []DPFkey) [][]byte {
+	if len(keys) == 0 {
+		return nil
+	}
+	kl := len(keys[0])
+	packed := make([]byte, kl*len(keys))
+	for i, k := range keys {
+		if len(k) != kl {
+			panic("dpf: keys of different lengths in one batch")
+		}
+		copy(packed[i*kl:], k)
+	}
+	flat := make([]byte, 32*len(keys))
+	check(C.dpf_pir_answer(p.h, u8(packed), C.size_t(kl), C.size_t(len(keys)), u8(flat)))
+	out := make([][]byte, len(keys))
+	for i := range out {
+		out[i] = flat[i*32 : (i+1)*32 : (i+1)*32]
+	}
+	return out
+}
+
+// Close frees the GPU copies of the database.
+func (p *PirDB) Close() {
+	if p.h != nil {
+		C.dpf_pir_db_free(p.h)
+		p.h = nil
+	}
+}

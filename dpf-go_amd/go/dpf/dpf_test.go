@@ -45,6 +45,26 @@ func TestGenPanics(t *testing.T) {
 	Gen(8, 3)
 }
 
+// Two servers' PIR answers XOR to the queried record.
+func TestPirTwoServer(t *testing.T) {
+	const logN = uint64(12)
+	db := make([]byte, 32<<logN)
+	for i := range db {
+		db[i] = byte(i*131 + i>>8)
+	}
+	p := NewPirDB(db, logN, 1)
+	defer p.Close()
+	for _, alpha := range []uint64{0, 1, 777, 1<<logN - 1} {
+		a, b := Gen(alpha, logN)
+		ra, rb := p.Answer([]DPFkey{a}), p.Answer([]DPFkey{b})
+		for j := 0; j < 32; j++ {
+			if ra[0][j]^rb[0][j] != db[32*alpha+uint64(j)] {
+				t.Fatalf("alpha=%d byte %d", alpha, j)
+			}
+		}
+	}
+}
+
 func BenchmarkEvalFull20(b *testing.B) {
 	k, _ := Gen(0, 20)
 	b.ResetTimer()

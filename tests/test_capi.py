@@ -76,6 +76,17 @@ def test_key_pack_rejects_ragged_batches():
         dpf.keys_pack([ka], key_len=len(ka) + 1)
 
 
+def test_xor_fold_validates_before_touching_a_device():
+    """dpf_xor_fold_dev rejects bad shapes with DPF_ERR_PARAM (no GPU needed:
+    validation precedes any device call); pointers are never dereferenced."""
+    L = dpf.lib()
+    p = 4096   # aligned fake device address, never used
+    for stride, nrec, rec in ((16, 128, 48), (16, 128, 0), (24, 8, 32), (16, 129, 32)):
+        assert L.dpf_xor_fold_dev(0, p, stride, 1, p, nrec, rec, p, p, None) == dpf.DPF_ERR_PARAM
+    assert L.dpf_xor_fold_dev(0, p + 4, 16, 1, p, 128, 32, p, p, None) == dpf.DPF_ERR_PARAM   # misaligned bits
+    assert dpf.xor_fold_workspace_size() > 0
+
+
 def test_batch_gen_matches_single():
     logN = 20
     al, s0, s1 = synth.key_seeds(64, logN)
