@@ -71,7 +71,8 @@ def load_peaks() -> dict:
             "lds_lookups_Gs": float(d.get("ds_read_b32_lookup_G_per_s", 16438.3))}
 
 
-def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, aes_impl: str = "lds-ttable") -> dict:
+def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, aes_impl: str = "lds-ttable",
+                 workload: str = "evalfull") -> dict:
     """PRG roofline: 22,928 two-input gate-equivalents per
     AES-MMO block against the guide's VALU issue rate x 32 bit-lanes x 2
     gates per v_bitop3 (5.03 P gate-eq/s).  `lds` is the T-table back end's
@@ -105,6 +106,20 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
                     "peak_measured": round(peaks["lds_lookups_Gs"] / 1e3, 3)}
     # Measured HBM bytes per launch of this kernel from the committed PMC
     # passes (tools/counters.sh + tools/traffic.py -> profiles/*traffic.json).
+    # Multi-kernel steps (eval, pir) sum every dpf kernel of their own PMC
+    # run (one launch of each per step).
+    if workload != "evalfull":
+        try:
+            with open(os.path.join(ROOT, "profiles", f"r02_traffic_{workload}.json")) as f:
+                t = json.load(f)
+            ks = sorted(k for k in t if k.startswith("k_"))
+            tot = sum(t[k]["traffic_bytes"] for k in ks)
+            r["traffic"] = round(tot)
+            r["traffic_over_algorithmic"] = round(tot / hbm_bytes, 3)
+            r["traffic_source"] = f"profiles/r02_traffic_{workload}.json (sum of {', '.join(ks)})"
+        except Exception:
+            pass
+        return r
     for name in ("r02_traffic.json", "r01_traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
@@ -403,8 +418,13 @@ def wl_eval(c: Ctx) -> dict:
                   config={"workload": f"batched Eval, {nk} keys x {ppk} points, logN={logN} per GPU "
                                       f"(BASELINE configs[2])", "logN": logN, "parallelism": f"key-shard x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes_done / (k_ms * 1e-3), "k_unpack+[k_evalfull<nodes>]+k_eval", k_ms,
-                                    q * 9 + nk * (stop_of(logN) + 2) * 32)
+    line["roofline"] = prg_roofline(aes_done / (k_ms * 1e-3), "k_unpack+[k_evalfull<nodes>]+k_eval", k_ms, 
+                                    q * 9 + nk * (stop_of(logN) + 2) * 32, workload="eval")
+    if L:
+        fb = nk * (1 << L) * 17 + q * 17
+        line["roofline"]["frontier_bytes"] = fb
+        line["roofline"]["frontier_note"] = ("the HBM frontier trades AES for bytes: 17 B per node written once and "
+                                             "17 B read per query, not part of the algorithmic 9 B per query")
     line["roofline"]["note"] = (f"achieved counts the AES the kernels compute: a shared frontier at level {L} "
                                 f"(2^(L+1)-2 per key) + stop-L+1 per query = {aes_done / q:.2f} per query, against "
                                 f"the per-query walk's {stop_of(logN) + 1} (aes_blocks_per_s above)")
@@ -453,7 +473,7 @@ def wl_split(c: Ctx) -> dict:
                                       + " (BASELINE configs[3])",
                                                 "logN": logN, "parallelism": f"subtree-split x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7, false, false>", k_ms, part)
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7, false, false>", k_ms, part, workload="split")
     return line
 
 
@@ -506,8 +526,8 @@ def wl_pir(c: Ctx) -> dict:
                                       + " (BASELINE configs[4])", "logN": logN, "batch": nk,
                           "parallelism": f"db-shard x{c.world} + all_gather/XOR"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_evalfull+k_pir_fold", k_ms,
-                                    (hi - lo) * 32 + nk * ((hi - lo) // 8) * 2)
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_evalfull+k_pir_fold", k_ms, 
+                                    (hi - lo) * 32 + nk * ((hi - lo) // 8) * 2, workload="pir")
     return line
 
 

@@ -144,6 +144,23 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         store16(c.outp + 32, leaf_fix(o2, RL.t, c.fcw));
         store16(c.outp + 48, leaf_fix(o3, RR.t, c.fcw));
         c.outp += 64;
+    } else if constexpr (D == 2 && NODES) {
+        // Bottom two levels of a frontier at once: 4 seeds = 64 contiguous
+        // bytes and their 4 t bytes as one 32-bit store (one byte store per
+        // node made the NODES pass write 2.2x its 17 B per node).
+        CW cw = load_cw(c.ek, lvl0 + DMAX - 2);
+        Node L, R;
+        expand(c.tab, c.lo, n, cw, L, R);
+        CW cw1 = load_cw(c.ek, lvl0 + DMAX - 1);
+        Node q[4];
+        expand(c.tab, c.lo, L, cw1, q[0], q[1]);
+        expand(c.tab, c.lo, R, cw1, q[2], q[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c.nseed[i] = make_uint4(q[i].s.c0, q[i].s.c1, q[i].s.c2, q[i].s.c3);
+        *reinterpret_cast<uint32_t*>(c.nt) = (q[0].t & 0xffu) | ((q[1].t & 0xffu) << 8) | ((q[2].t & 0xffu) << 16) |
+                                             ((q[3].t & 0xffu) << 24);
+        c.nseed += 4;
+        c.nt += 4;
     } else if constexpr (D == 1) {
         CW cw = load_cw(c.ek, lvl0 + DMAX - 1);
         Node L, R;

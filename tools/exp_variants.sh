@@ -7,7 +7,7 @@ REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$REPO"
 OUT="gpurun_out/$1"; shift
 mkdir -p "$OUT"
-B=(--steps 50 --warmup 10 --no-cpu-baseline --no-variants --no-api --aes ttable)
+B=(--steps 50 --warmup 10 --spinup 0.5 --no-cpu-baseline --no-variants --no-api --aes ttable)
 lib() { if [ "$1" = base ]; then echo "$REPO/dpf-go_amd/lib/libdpf_hip.so"; else echo "$REPO/dpf-go_amd/lib/variants/libdpf_hip_$1.so"; fi; }
 for r in 1 2; do
   for v in "$@"; do

@@ -14,5 +14,9 @@ for w in eval split pir; do
   ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$REPO/gpurun_out/$T/kt_$w" -o kt --output-format csv -- \
       python3 "$REPO/bench.py" --workload $w --steps 20 --warmup 5 > "$REPO/gpurun_out/$T/kt_$w.log" 2>&1 ) || { echo "kt $w failed"; exit 1; }
 done
+for w in eval split pir; do
+  bash tools/counters.sh "gpurun_out/$T/pmc_$w" $w > /dev/null 2>&1 || { echo "pmc $w failed"; exit 1; }
+  python3 tools/traffic.py "gpurun_out/$T/pmc_$w/summary.json" "gpurun_out/$T/traffic_$w.json" > /dev/null
+done
 { command -v go && go version; } > "gpurun_out/$T/go_probe.txt" 2>&1 || echo "go: not found on the GPU box ($(date -u +%FT%TZ))" > "gpurun_out/$T/go_probe.txt"
 echo "round profile done"
