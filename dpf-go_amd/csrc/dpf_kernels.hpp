@@ -42,7 +42,8 @@ hipError_t launch_nodes(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint3
                         uint64_t prefix, uint8_t* seeds, uint8_t* ts, uint64_t stride, hipStream_t st);
 
 // Batched Eval.  When a key has enough points to share the top of its tree
-// (2^(L+2) <= pts_per_key), the 2^L nodes at level L of every key are first
+// (L = the deepest level with 2^(L+1) <= pts_per_key, used when L >= 4), the
+// 2^L nodes at level L of every key are first
 // computed into `frontier` (eval_frontier_bytes of it) and each query starts
 // there; with frontier == nullptr (or too small) every walk starts at the root.
 uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key);
