@@ -69,6 +69,58 @@ __global__ void k_unpack_bs(const uint8_t* __restrict__ keys, uint64_t key_len, 
     }
 }
 
+// Both back ends' key records in one launch, one thread per output word
+// (the tree workspace holds both, so either back end can run from one
+// expansion): record r of a key has 8 T-table words (k_unpack's layout,
+// dpf_kernels.hip) and, for r >= 1, the byte-sliced record r-1 (36 words;
+// 32 for the final CW).  Replaces k_unpack + k_unpack_bs (2 launches, one
+// thread per record) on the tree paths.
+constexpr uint32_t kUnpackWords = 8 + kBsRec;
+__global__ void k_unpack_both(const uint8_t* __restrict__ keys, uint64_t key_len, uint64_t nkeys, uint32_t stop,
+                              uint32_t* __restrict__ ek, uint32_t* __restrict__ ekb) {
+    const uint64_t recs = (uint64_t)stop + 2;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nkeys * recs * kUnpackWords) return;
+    const uint64_t k = i / (recs * kUnpackWords), rem = i % (recs * kUnpackWords);
+    const uint32_t r = (uint32_t)(rem / kUnpackWords), w = (uint32_t)(rem % kUnpackWords);
+    const uint8_t* kp = keys + k * key_len;
+    // byte source of record r: root (dpf.go:244-246), level r-1 CW (:231-233), final CW at len-16 (:206,219)
+    const uint8_t* p = r == 0 ? kp : r <= stop ? kp + 17 + 18 * (r - 1) : kp + key_len - 16;
+    if (w < 8) {
+        uint32_t v = 0;
+        if (w < 4) {
+            v = (uint32_t)p[4 * w] | ((uint32_t)p[4 * w + 1] << 8) | ((uint32_t)p[4 * w + 2] << 16) |
+                ((uint32_t)p[4 * w + 3] << 24);
+        } else if (w == 4 && r <= stop) {
+            v = p[16];                                   // root t / tLCW
+        } else if (w == 5 && r >= 1 && r <= stop) {
+            v = p[17];                                   // tRCW
+        }
+        ek[k * (recs * 8) + r * 8 + w] = v;
+        return;
+    }
+    if (r == 0) return;                                  // the root has no byte-sliced record
+    const uint32_t rb = r - 1, j = w - 8;                // rb == stop: the final CW
+    if (rb == stop && j >= 32) return;
+    uint32_t v;
+    if (j < 32) {
+        v = planes_word(p, j >> 3, j & 7);
+    } else {
+        const uint8_t t = p[16 + ((j - 32) >> 1)];      // tLCW for 32/33, tRCW for 34/35
+        v = (j & 1) ? (t > 1 ? ~0u : 0u) : (t == 1 ? ~0u : 0u);
+    }
+    ekb[k * bs_key_words(stop) + (uint64_t)rb * kBsRec + j] = v;
+}
+
+hipError_t launch_unpack_both(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ek,
+                              uint32_t* ekb, hipStream_t st) {
+    const uint64_t n = nkeys * ((uint64_t)stop + 2) * kUnpackWords;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpack_both, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, keys, key_len, nkeys, stop,
+                       ek, ekb);
+    return hipGetLastError();
+}
+
 // Child set after aes_mmo8 (o = MMO(x)): split the control bits off (byte 0
 // of row 0 / plane 0), clear them, apply the parent's correction (dpf.go:
 // 61-68,230-238).  tp: parent "t != 0" mask (bit i of every byte = block i).

@@ -45,6 +45,9 @@ bool bs_applicable(uint32_t stop, uint32_t prefix_bits);
 uint32_t bs_depth(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits);
 uint64_t bs_frontier_bytes(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits);
 
+// T-table records (ek, k_unpack's layout) and byte-sliced records (ekb) in one launch.
+hipError_t launch_unpack_both(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ek,
+                              uint32_t* ekb, hipStream_t st);
 hipError_t launch_unpack_bs(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ekb,
                             hipStream_t st);
 // EvalFull of subtree (prefix_bits, prefix) of every key through the

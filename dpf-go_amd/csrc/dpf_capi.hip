@@ -372,9 +372,7 @@ TreeWs tree_ws(void* work, size_t nk, uint32_t stop) {
 
 // Key records for both back ends (the byte-sliced words are 3% of a tree launch at configs[1]).
 hipError_t expand_keys(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t stop, const TreeWs& w, hipStream_t st) {
-    hipError_t e = dpfk::launch_unpack(d_keys, klen, nk, stop, w.ek, st);
-    if (e != hipSuccess) return e;
-    return dpfk::launch_unpack_bs(d_keys, klen, nk, stop, w.ekb, st);
+    return dpfk::launch_unpack_both(d_keys, klen, nk, stop, w.ek, w.ekb, st);
 }
 
 // Leaves of subtree (prefix_bits, prefix) of keys [k0, k0 + n) through the selected back end.
