@@ -19,6 +19,10 @@
 #include "aes_ttable.hpp"
 #include "dpf_kernels.hpp"
 
+#ifndef DPF_PAIR_STORES
+#define DPF_PAIR_STORES 1
+#endif
+
 namespace dpfk {
 
 struct Node {
@@ -109,14 +113,65 @@ __device__ __forceinline__ void emit_node(Ctx& c, const Node& n) {
     *c.nt++ = (uint8_t)n.t;
 }
 
+// Exchange a value with the other lane of the pair (lane ^ 1): DPP
+// quad_perm [1,0,3,2], VALU only (no LDS traffic; the T-table owns the LDS).
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ Node pair_swap(const Node& n) {
+    return {{pair_swap(n.s.c0), pair_swap(n.s.c1), pair_swap(n.s.c2), pair_swap(n.s.c3)}, pair_swap(n.t)};
+}
+__device__ __forceinline__ Node sel(bool b, const Node& x, const Node& y) {
+    return {{b ? x.s.c0 : y.s.c0, b ? x.s.c1 : y.s.c1, b ? x.s.c2 : y.s.c2, b ? x.s.c3 : y.s.c3}, b ? x.t : y.t};
+}
+
+// Bottom two levels below node n: 4 leaves = 64 contiguous bytes at p
+// (dpf.go:214-224 for each), expanded together and stored back to back.
+__device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& n, uint8_t* p) {
+    CW cw = load_cw(c.ek, lvl);
+    Node L, R;
+    expand(c.tab, c.lo, n, cw, L, R);
+    CW cw1 = load_cw(c.ek, lvl + 1);
+    Node LL, LR, RL, RR;
+    expand(c.tab, c.lo, L, cw1, LL, LR);
+    expand(c.tab, c.lo, R, cw1, RL, RR);
+    Blk o0, o1, o2, o3;
+    mmo_pair(c.tab, c.lo, KeyFixed<false>{}, LL.s, o0, KeyFixed<false>{}, LR.s, o1);
+    mmo_pair(c.tab, c.lo, KeyFixed<false>{}, RL.s, o2, KeyFixed<false>{}, RR.s, o3);
+    store16(p, leaf_fix(o0, LL.t, c.fcw));
+    store16(p + 16, leaf_fix(o1, LR.t, c.fcw));
+    store16(p + 32, leaf_fix(o2, RL.t, c.fcw));
+    store16(p + 48, leaf_fix(o3, RR.t, c.fcw));
+}
+
 // Depth-first expansion of D more levels below node n at tree level `lvl0 +
 // (DMAX - D)`; the right child of every internal node stays live in
 // registers while the left subtree is expanded.  Leaf mode writes the
 // converted leaves (dpf.go:214-224); node mode (NODES) writes the 2^D nodes
 // D levels down instead: the frontier a batched Eval continues from.
-template <int DMAX, int D, bool NODES>
+template <int DMAX, int D, bool NODES, bool PAIR>
 __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
-    if constexpr (D == 0) {
+    if constexpr (PAIR && D == 3) {
+        // Lane pairs write whole 128-B lines.  Lanes 2i and 2i+1 own adjacent
+        // subtrees a and b of one key (same CWs), 16 << DMAX bytes apart, and
+        // reach their depth-3 nodes Na, Nb in lockstep.  After expanding, the
+        // even lane trades R(Na) for the odd lane's L(Nb): first the pair
+        // computes Na's 8 leaves (even: 0-3, odd: 4-7) and stores the line in
+        // one instruction, then Nb's.  Storing a line as two 64-B halves 8 AES
+        // apart left ~4 MiB of half-written lines per XCD (its whole L2) and
+        // made WRITE_SIZE 1.26x the output.  Leaves are unchanged, only which
+        // lane computes them.
+        CW cw = load_cw(c.ek, lvl0 + DMAX - 3);
+        Node L, R;
+        expand(c.tab, c.lo, n, cw, L, R);
+        const bool odd = (threadIdx.x & 1u) != 0;
+        const Node got = pair_swap(sel(odd, L, R));   // even gets L(Nb), odd gets R(Na)
+        const int64_t sub = 16ll << DMAX;
+        const Node first = sel(odd, got, L), second = sel(odd, R, got);
+        leaves4(c, lvl0 + DMAX - 2, first, c.outp + (odd ? 64 - sub : 0));
+        leaves4(c, lvl0 + DMAX - 2, second, c.outp + (odd ? 64 : sub));
+        c.outp += 128;
+    } else if constexpr (D == 0) {
         if constexpr (NODES) {
             emit_node(c, n);
         } else {
@@ -126,23 +181,8 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         }
     } else if constexpr (D == 2 && !NODES) {
         // Bottom two levels at once: 4 leaves = 64 contiguous bytes stored back
-        // to back.  Pairs of 32-B stores three AES apart left partial lines to
-        // be written twice: WRITE_SIZE 1.47x -> 1.28x the 512 MiB output, 1%
-        // faster (profiles/r02/variants).
-        CW cw = load_cw(c.ek, lvl0 + DMAX - 2);
-        Node L, R;
-        expand(c.tab, c.lo, n, cw, L, R);
-        CW cw1 = load_cw(c.ek, lvl0 + DMAX - 1);
-        Node LL, LR, RL, RR;
-        expand(c.tab, c.lo, L, cw1, LL, LR);
-        expand(c.tab, c.lo, R, cw1, RL, RR);
-        Blk o0, o1, o2, o3;
-        mmo_pair(c.tab, c.lo, KeyFixed<false>{}, LL.s, o0, KeyFixed<false>{}, LR.s, o1);
-        mmo_pair(c.tab, c.lo, KeyFixed<false>{}, RL.s, o2, KeyFixed<false>{}, RR.s, o3);
-        store16(c.outp, leaf_fix(o0, LL.t, c.fcw));
-        store16(c.outp + 16, leaf_fix(o1, LR.t, c.fcw));
-        store16(c.outp + 32, leaf_fix(o2, RL.t, c.fcw));
-        store16(c.outp + 48, leaf_fix(o3, RR.t, c.fcw));
+        // to back (subtrees too shallow or lanes of different keys for PAIR).
+        leaves4(c, lvl0 + DMAX - 2, n, c.outp);
         c.outp += 64;
     } else if constexpr (D == 2 && NODES) {
         // Bottom two levels of a frontier at once: 4 seeds = 64 contiguous
@@ -187,7 +227,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
             ch.s.c2 = side ? R.s.c2 : L.s.c2;
             ch.s.c3 = side ? R.s.c3 : L.s.c3;
             ch.t = side ? R.t : L.t;
-            dfs<DMAX, D - 1, NODES>(c, lvl0, ch);
+            dfs<DMAX, D - 1, NODES, PAIR>(c, lvl0, ch);
         }
     }
 }
@@ -258,7 +298,11 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
         CW cw = load_cw(ek, i);
         walk_step(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
-    dfs<D, D, NODES>(c, ltop, n);
+    // Lane pairs share a key when a wave owns one key (UNIFORM): whole-line
+    // leaf stores (dfs PAIR).  DPF_PAIR_STORES=0 builds the r02 half-line
+    // stores for A/B runs.
+    constexpr bool kPair = DPF_PAIR_STORES && UNIFORM && !NODES && D >= 3;
+    dfs<D, D, NODES, kPair>(c, ltop, n);
 }
 
 // Batched Eval: one thread per query, independent walks that compute only
