@@ -54,7 +54,10 @@ __device__ __forceinline__ Blk load_blk(const uint32_t* p) {
 // The two independent MMOs of a PRG call (or of a leaf pair), written as two
 // plain mmo1 calls so the scheduler interleaves them freely: 98.9 G blocks/s
 // in tools/aes_variants.hip, against 88.4 for a round-by-round interleave
-// and 93.3 fully serialized (r01 A/B, profiles/r01/full_ilp*).
+// and 93.3 fully serialized (r01 A/B, profiles/r01/full_ilp*).  An explicit
+// software pipeline (each block's 16 lookups issued while the other block's
+// are in flight, up to 32 per wave) was slower again: 93.1 vs 93.8 in-tree,
+// 21 VGPRs spilled (profiles/r02/pipe).
 template <class KA, class KB>
 __device__ __forceinline__ void mmo_pair(const uint8_t* tab, uint32_t lo, const KA& ka, Blk xa, Blk& oa,
                                          const KB& kb, Blk xb, Blk& ob) {
