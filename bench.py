@@ -473,7 +473,7 @@ def wl_split(c: Ctx) -> dict:
                                       + " (BASELINE configs[3])",
                                                 "logN": logN, "parallelism": f"subtree-split x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7, false, false>", k_ms, part, workload="split")
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7, true, false>", k_ms, part, workload="split")
     return line
 
 
