@@ -19,6 +19,9 @@
 #include "aes_ttable.hpp"
 #include "dpf_kernels.hpp"
 
+#ifndef DPF_COOP_WALK
+#define DPF_COOP_WALK 1
+#endif
 #ifndef DPF_PAIR_STORES
 #define DPF_PAIR_STORES 1
 #endif
@@ -297,7 +300,38 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     Node n;
     n.s = load_blk(ek);
     n.t = ek[4];
-    for (uint32_t i = 0; i < ltop; ++i) {
+    uint32_t lvl = 0;
+    if constexpr (UNIFORM) {
+        // Shared walk: when the whole workgroup (B = 2^W threads) evaluates
+        // consecutive subtrees of one key, its threads' paths agree on the
+        // top ltop - W levels and fan out to B nodes below.  Wave 0 walks
+        // 64 paths down to level l1 = ltop - W + 6 (one per group of B/64
+        // threads) and leaves them in LDS; every thread then walks only the
+        // last W - 6 levels.  Wave-AES per workgroup: l1 + (B/64)(W - 6)
+        // instead of (B/64) ltop (configs[4]: 33 vs 96, configs[3]: 39 vs 144).
+        __shared__ uint32_t s_front[64 * 5];
+        const uint32_t B = blockDim.x;
+        const uint32_t W = 31u - (uint32_t)__builtin_clz(B);
+        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W) {   // uniform over the workgroup
+            const uint32_t l1 = ltop - W + 6;
+            if (threadIdx.x < 64) {
+                const uint64_t subj = (sub - threadIdx.x) + ((uint64_t)threadIdx.x << (W - 6));
+                Node m = n;
+                for (uint32_t i = 0; i < l1; ++i) {
+                    CW cw = load_cw(ek, i);
+                    walk_step(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
+                }
+                uint32_t* f = s_front + 5 * threadIdx.x;
+                f[0] = m.s.c0; f[1] = m.s.c1; f[2] = m.s.c2; f[3] = m.s.c3; f[4] = m.t;
+            }
+            __syncthreads();
+            const uint32_t* f = s_front + 5 * (threadIdx.x >> (W - 6));
+            n.s = {f[0], f[1], f[2], f[3]};
+            n.t = f[4];
+            lvl = l1;
+        }
+    }
+    for (uint32_t i = lvl; i < ltop; ++i) {
         CW cw = load_cw(ek, i);
         walk_step(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
