@@ -250,11 +250,21 @@ class Ctx:
         # 1.069 ms after 60 steps (profiles/r02/warmup).  Steady state is what
         # a busy server sees, so every workload first runs its own step for
         # SPINUP_S seconds of wall time.
+        # Ranks agree on when to stop (MIN over ranks of "still spinning"):
+        # a step may hold a collective (PIR's gather), so every rank must run
+        # the same number of spin-up steps.
         t_spin = time.perf_counter()
-        while time.perf_counter() - t_spin < self.args.spinup:
+        more = self.args.spinup > 0
+        while more:
             for _ in range(4):
                 step(None)
             torch.cuda.synchronize(self.dev)
+            more = time.perf_counter() - t_spin < self.args.spinup
+            if self.world > 1:
+                f = torch.tensor([1.0 if more else 0.0], dtype=torch.float64,
+                                 device=self.dev if self.backend == "nccl" else "cpu")
+                dist.all_reduce(f, op=dist.ReduceOp.MIN)
+                more = float(f.item()) > 0
         for _ in range(warmup):
             step(None)
         torch.cuda.synchronize(self.dev)
