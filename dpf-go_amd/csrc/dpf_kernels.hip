@@ -25,6 +25,9 @@
 #ifndef DPF_PAIR_STORES
 #define DPF_PAIR_STORES 1
 #endif
+#ifndef DPF_MMO_INTERLEAVE
+#define DPF_MMO_INTERLEAVE 1
+#endif
 
 namespace dpfk {
 
@@ -64,8 +67,12 @@ __device__ __forceinline__ Blk load_blk(const uint32_t* p) {
 template <class KA, class KB>
 __device__ __forceinline__ void mmo_pair(const uint8_t* tab, uint32_t lo, const KA& ka, Blk xa, Blk& oa,
                                          const KB& kb, Blk xb, Blk& ob) {
+#if DPF_MMO_INTERLEAVE
+    mmo2(tab, lo, ka, xa, oa, kb, xb, ob);
+#else
     oa = mmo1(tab, lo, ka, xa);
     ob = mmo1(tab, lo, kb, xb);
+#endif
 }
 
 __device__ __forceinline__ void expand(const uint8_t* tab, uint32_t lo, const Node& n, const CW& cw, Node& L,
@@ -131,23 +138,42 @@ __device__ __forceinline__ Node sel(bool b, const Node& x, const Node& y) {
     return {{b ? x.s.c0 : y.s.c0, b ? x.s.c1 : y.s.c1, b ? x.s.c2 : y.s.c2, b ? x.s.c3 : y.s.c3}, b ? x.t : y.t};
 }
 
+__device__ __forceinline__ Blk bsel(bool b, const Blk& x, const Blk& y) {
+    return {b ? x.c0 : y.c0, b ? x.c1 : y.c1, b ? x.c2 : y.c2, b ? x.c3 : y.c3};
+}
+
 // Bottom two levels below node n: 4 leaves = 64 contiguous bytes at p
-// (dpf.go:214-224 for each), expanded together and stored back to back.
+// (dpf.go:214-224 for each), stored back to back once all four are done.
+// The two children are finished by one loop body (expand + leaf pair), not
+// two inlined copies: the tree kernel's innermost loop must fit the
+// instruction cache (64 KiB per two CUs).  Fully inlined, the PAIR path's
+// loop body was ~85 KiB of code (22 AES-MMO bodies).
 __device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& n, uint8_t* p) {
     CW cw = load_cw(c.ek, lvl);
     Node L, R;
     expand(c.tab, c.lo, n, cw, L, R);
     CW cw1 = load_cw(c.ek, lvl + 1);
-    Node LL, LR, RL, RR;
-    expand(c.tab, c.lo, L, cw1, LL, LR);
-    expand(c.tab, c.lo, R, cw1, RL, RR);
-    Blk o0, o1, o2, o3;
-    mmo_pair(c.tab, c.lo, KeyFixed<false>{}, LL.s, o0, KeyFixed<false>{}, LR.s, o1);
-    mmo_pair(c.tab, c.lo, KeyFixed<false>{}, RL.s, o2, KeyFixed<false>{}, RR.s, o3);
-    store16(p, leaf_fix(o0, LL.t, c.fcw));
-    store16(p + 16, leaf_fix(o1, LR.t, c.fcw));
-    store16(p + 32, leaf_fix(o2, RL.t, c.fcw));
-    store16(p + 48, leaf_fix(o3, RR.t, c.fcw));
+    Blk o0 = {}, o1 = {}, o2, o3;
+#pragma nounroll
+    for (int h = 0; h < 2; ++h) {
+        const Node m = sel(h == 0, L, R);
+        Node a, b;
+        expand(c.tab, c.lo, m, cw1, a, b);
+        Blk oa, ob;
+        mmo_pair(c.tab, c.lo, KeyFixed<false>{}, a.s, oa, KeyFixed<false>{}, b.s, ob);
+        oa = leaf_fix(oa, a.t, c.fcw);
+        ob = leaf_fix(ob, b.t, c.fcw);
+        o2 = oa;
+        o3 = ob;
+        if (h == 0) {
+            o0 = oa;
+            o1 = ob;
+        }
+    }
+    store16(p, o0);
+    store16(p + 16, o1);
+    store16(p + 32, o2);
+    store16(p + 48, o3);
 }
 
 // Depth-first expansion of D more levels below node n at tree level `lvl0 +
@@ -174,8 +200,10 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         const Node got = pair_swap(sel(odd, L, R));   // even gets L(Nb), odd gets R(Na)
         const int64_t sub = 16ll << DMAX;
         const Node first = sel(odd, got, L), second = sel(odd, R, got);
-        leaves4(c, lvl0 + DMAX - 2, first, c.outp + (odd ? 64 - sub : 0));
-        leaves4(c, lvl0 + DMAX - 2, second, c.outp + (odd ? 64 : sub));
+#pragma nounroll
+        for (int h = 0; h < 2; ++h)   // one code copy of leaves4 (instruction cache)
+            leaves4(c, lvl0 + DMAX - 2, sel(h == 0, first, second),
+                    c.outp + (h == 0 ? (odd ? 64 - sub : 0) : (odd ? 64 : sub)));
         c.outp += 128;
     } else if constexpr (D == 0) {
         if constexpr (NODES) {
