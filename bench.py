@@ -72,7 +72,7 @@ def load_peaks() -> dict:
 
 
 def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, aes_impl: str = "lds-ttable",
-                 workload: str = "evalfull") -> dict:
+                 workload: str = "evalfull", profiled_shape: bool = True) -> dict:
     """PRG roofline: 22,928 two-input gate-equivalents per
     AES-MMO block against the guide's VALU issue rate x 32 bit-lanes x 2
     gates per v_bitop3 (5.03 P gate-eq/s).  `lds` is the T-table back end's
@@ -107,20 +107,28 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
     # Measured HBM bytes per launch of this kernel from the committed PMC
     # passes (tools/counters.sh + tools/traffic.py -> profiles/*traffic.json).
     # Multi-kernel steps (eval, pir) sum every dpf kernel of their own PMC
-    # run (one launch of each per step).
+    # run (one launch of each per step).  Only when those passes profiled
+    # this per-rank shape (profiled_shape): a split/PIR rank of an N-way
+    # split runs a 1/N-size subtree, which no committed profile measured.
+    if not profiled_shape:
+        r["traffic_note"] = "no PMC profile at this per-rank shape (1/N of the 1-GPU split); traffic not reported"
+        return r
     if workload != "evalfull":
-        try:
-            with open(os.path.join(ROOT, "profiles", f"r02_traffic_{workload}.json")) as f:
-                t = json.load(f)
+        for rnd in ("r03", "r02"):
+            name = f"{rnd}_traffic_{workload}.json"
+            try:
+                with open(os.path.join(ROOT, "profiles", name)) as f:
+                    t = json.load(f)
+            except Exception:
+                continue
             ks = sorted(k for k in t if k.startswith("k_"))
             tot = sum(t[k]["traffic_bytes"] for k in ks)
             r["traffic"] = round(tot)
             r["traffic_over_algorithmic"] = round(tot / hbm_bytes, 3)
-            r["traffic_source"] = f"profiles/r02_traffic_{workload}.json (sum of {', '.join(ks)})"
-        except Exception:
-            pass
+            r["traffic_source"] = f"profiles/{name} (sum of {', '.join(ks)})"
+            break
         return r
-    for name in ("r02_traffic.json", "r01_traffic.json"):
+    for name in ("r03_traffic.json", "r02_traffic.json", "r01_traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 t = json.load(f)
@@ -224,6 +232,7 @@ class Ctx:
         # the control-plane collectives go over gloo (RCCL refuses two ranks
         # on one GPU).  DPF_BENCH_BACKEND overrides.
         ndev = max(1, torch.cuda.device_count())
+        self.folded = self.world > ndev          # a rehearsal, not an N-GPU measurement
         self.backend = os.environ.get("DPF_BENCH_BACKEND", "nccl" if self.world <= ndev else "gloo")
         self.local = int(os.environ.get("LOCAL_RANK", "0")) % ndev
         if self.world > 1:
@@ -483,24 +492,53 @@ def wl_split(c: Ctx) -> dict:
                                       + " (BASELINE configs[3])",
                                                 "logN": logN, "parallelism": f"subtree-split x{c.world}"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7, true, false>", k_ms, part, workload="split")
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_evalfull<7, true, false>", k_ms, part, workload="split",
+                                    profiled_shape=(W == 1))
+    if c.world == 1 and not a.no_api:
+        line["api"] = split_api_rate(c, ka[0].tobytes(), logN)
     return line
 
 
-def wl_pir(c: Ctx) -> dict:
-    a, dpf, torch = c.args, c.dpf, c.torch
+def split_api_rate(c: Ctx, key: bytes, logN: int, reps: int = 3) -> dict:
+    """configs[3] through the host-buffer C ABI dpf_evalfull_split (key H2D,
+    the whole 2^(logN-3)-byte output D2H into caller memory, synchronous):
+    what a Go EvalFull caller gets (dpf.go:251 returns the whole slice).
+    Into a REUSED caller buffer; median of `reps` calls."""
+    dpf = c.dpf
+    out = np.empty(dpf.evalfull_len(logN), np.uint8)
+    dpf.evalfull_split(key, logN, 1, out=out)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dpf.evalfull_split(key, logN, 1, out=out)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"entry": "dpf_evalfull_split (host buffer, synchronous, 1 GPU)", "bytes_out": out.nbytes,
+            "reused_out": {"ms": round(t * 1e3, 3), "points_per_s": (1 << logN) / t,
+                           "D2H_GBs": round(out.nbytes / t / 1e9, 2)}}
+
+
+def pir_setup(c: Ctx, W: int):
+    """This rank's DB slice in HBM (the same synthetic DB on every run)."""
     from dpf import synth, shard
-    logN, nk = a.pir_logN, a.batch
+    logN = c.args.pir_logN
     nrec = 1 << logN
-    kl = dpf.key_len(logN)
-    W = c.world if c.world > 1 else max(1, a.emulate_world)
-    pb, prefix = shard.subtree_split(W, c.rank)
     lo, hi = shard.db_slice(nrec, logN, W, c.rank)
     db = synth.db_bytes(hi * 32)[lo * 32:]                    # this rank's slice of the synthetic DB
+    return c.torch.from_numpy(db).to(c.dev), lo, hi
+
+
+def pir_time(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int, warmup: int):
+    """Time `steps` PIR steps of nk queries: server answers on this GPU's
+    slice (dpf_pir_answer_dev), then the gather + host XOR when world > 1."""
+    dpf, torch = c.dpf, c.torch
+    from dpf import synth, shard
+    logN = c.args.pir_logN
+    kl = dpf.key_len(logN)
+    pb, prefix = shard.subtree_split(W, c.rank)
     al, s0, s1 = synth.key_seeds(nk, logN, first=4242)       # the same queries on every server GPU
     ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
     d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
-    d_db = torch.from_numpy(db).to(c.dev)
     d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=c.dev)
     d_work = torch.empty(dpf.pir_workspace_size(nk, logN, pb), dtype=torch.uint8, device=c.dev)
     result = {}
@@ -517,7 +555,18 @@ def wl_pir(c: Ctx) -> dict:
         else:
             result["ans"] = d_ans.view(nk, 32).cpu().numpy()
 
-    t_wall, k_ms = c.timed(step, a.steps, a.warmup)
+    t_wall, k_ms = c.timed(step, steps, warmup)
+    return ka, result, t_wall, k_ms
+
+
+def wl_pir(c: Ctx) -> dict:
+    a, dpf = c.args, c.dpf
+    from dpf import synth
+    logN, nk = a.pir_logN, a.batch
+    nrec = 1 << logN
+    W = c.world if c.world > 1 else max(1, a.emulate_world)
+    d_db, lo, hi = pir_setup(c, W)
+    ka, result, t_wall, k_ms = pir_time(c, W, d_db, lo, hi, nk, a.steps, a.warmup)
     if a.check and c.rank == 0 and W == c.world:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
@@ -526,6 +575,7 @@ def wl_pir(c: Ctx) -> dict:
             want = oracle.pir_answer(ka[i].tobytes(), logN, full_db, 0, nrec)
             assert result["ans"][i].tobytes() == want, "PIR answer differs from oracle"
     sec = t_wall / a.steps
+    pb = (W - 1).bit_length()
     aes = nk * (3 * (1 << (stop_of(logN) - pb)) - 2)
     line = c.line(metric="2-server PIR answered queries/sec per server (EvalFull logN=24 + XOR fold)",
                   value=nk / sec, unit="queries/s", ms_per_step=sec * 1e3, scaling="strong",
@@ -536,8 +586,20 @@ def wl_pir(c: Ctx) -> dict:
                                       + " (BASELINE configs[4])", "logN": logN, "batch": nk,
                           "parallelism": f"db-shard x{c.world} + all_gather/XOR"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_evalfull+k_pir_fold", k_ms, 
-                                    (hi - lo) * 32 + nk * ((hi - lo) // 8) * 2, workload="pir")
+    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_evalfull+k_fold", k_ms,
+                                    (hi - lo) * 32 + nk * ((hi - lo) // 8) * 2, workload="pir",
+                                    profiled_shape=(W == 1 and nk == 64))
+    if c.world == 1 and not a.no_sweep:
+        # B in {1, 16, 64, 256}; the fold reads the DB once per
+        # batch up to 256 keys (pir_kernels.hip plan_fold).
+        sweep = {}
+        for b in (1, 16, 64, 256):
+            _, _, tw, km = pir_time(c, W, d_db, lo, hi, b, 20, 3)
+            sweep[str(b)] = {"ms_per_step": round(tw / 20 * 1e3, 4), "queries_per_s": b / (tw / 20),
+                             "kernel_ms": round(km, 4),
+                             "aes_blocks_per_s": b * (3 * (1 << (stop_of(logN) - pb)) - 2) / (km * 1e-3),
+                             "db_GBs": round((hi - lo) * 32 / (km * 1e-3) / 1e9, 1)}
+        line["batch_sweep"] = sweep
     return line
 
 
@@ -572,9 +634,17 @@ def dry_run(args) -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.barrier()
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "max_rank_s": float(t.item()), "local_ranks": os.environ.get("LOCAL_WORLD_SIZE")}),
-              flush=True)
+        # The line skeleton goes through the real policy code: traffic only
+        # for a profiled per-rank shape, cpu_baseline on rank 0 at every N.
+        wl = args.workload
+        same_shape = wl in ("evalfull", "eval") or world == 1
+        line = {"dry_run": True, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "max_rank_s": float(t.item()), "local_ranks": os.environ.get("LOCAL_WORLD_SIZE"),
+                "workload": wl, "scaling": "strong" if wl in ("split", "pir") else "weak"}
+        line["roofline"] = prg_roofline(1e11, "k_evalfull<7, true, false>", 1.0, 512 << 20, workload=wl,
+                                        profiled_shape=same_shape)
+        finalize(line, args, world, folded=False)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -599,6 +669,7 @@ def main() -> None:
                     help="tree-kernel AES back end for the headline (default: the library's)")
     ap.add_argument("--no-variants", action="store_true", help="skip timing the other AES back end")
     ap.add_argument("--no-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) API rates")
+    ap.add_argument("--no-sweep", action="store_true", help="pir: skip the B in {1,16,64,256} batch sweep")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--spinup", type=float, default=0.5,
                     help="seconds of untimed steps before the warmup (GPU clock ramp); 0 disables")
@@ -619,11 +690,23 @@ def main() -> None:
     c = Ctx(args)
     line = {"evalfull": wl_evalfull, "eval": wl_eval, "split": wl_split, "pir": wl_pir}[args.workload](c)
     if c.rank == 0:
-        if args.workload == "evalfull" and not args.no_cpu_baseline and c.world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.logN, args.cpu_seconds)
+        finalize(line, args, c.world, c.folded)
         print(json.dumps(line), flush=True)
     if c.world > 1:
         c.dist.destroy_process_group()
+
+
+def finalize(line: dict, args, world: int, folded: bool) -> None:
+    """Rank 0, after the timed region.  The headline carries the CPU
+    baseline at every N (taken after the timed steps, so it cannot perturb
+    them).  Ranks folded onto fewer GPUs than ranks are a rehearsal of the
+    N-rank plumbing, not an N-GPU number: marked, and no scaling class."""
+    if args.workload == "evalfull" and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.logN, args.cpu_seconds)
+    if folded:
+        line["folded_ranks"] = True
+        line["scaling"] = None
+        line["note"] = f"{world} ranks folded onto fewer GPUs (rehearsal): value is not an {world}-GPU rate"
 
 
 if __name__ == "__main__":

@@ -19,6 +19,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -235,8 +236,11 @@ class CopyPool {
 // g_mu, so dpf_gpu_shutdown only drops the registry's references: a call in
 // flight, or a PIR handle, keeps its devices alive until it is done with
 // them, and the last reference releases the device's buffers and streams.
+// The registry is a never-destroyed heap object: a process that exits
+// without dpf_gpu_shutdown runs no Dev destructor (so no HIP call) during
+// static teardown, whatever the order against the HIP runtime and torch.
 std::mutex g_mu;
-std::vector<std::shared_ptr<Dev>> g_devs;
+std::vector<std::shared_ptr<Dev>>& g_devs = *new std::vector<std::shared_ptr<Dev>>();
 
 struct DeviceGuard {
     int prev = -1;
@@ -404,11 +408,22 @@ int ensure_staging(Dev& d, size_t chunk_cap) {
     return DPF_OK;
 }
 
-// Large caller buffers (a fresh Go slice / numpy array): ask for
-// transparent huge pages, so first touch costs one fault per 2 MiB instead
-// of per 4 KiB (a no-op where THP is off or the pages already exist).
+// Opt-in (DPF_PREFAULT_OUTPUT=1): for large caller buffers (a fresh Go
+// slice / numpy array), ask for transparent huge pages and pre-touch the
+// pages in parallel while the GPU works, so first touch costs one fault per
+// 2 MiB instead of per 4 KiB inside the copy.  Off by default: it changes
+// the memory policy of caller-owned memory (a Go heap manages THP itself)
+// and zero-writes the buffer before data arrives.
+bool prefault_output() {
+    static const bool on = [] {
+        const char* e = getenv("DPF_PREFAULT_OUTPUT");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 void hint_hugepages(uint8_t* p, size_t n) {
-    if (n < ((size_t)64 << 20)) return;
+    if (n < ((size_t)64 << 20) || !prefault_output()) return;
     const uintptr_t a = ((uintptr_t)p + ((1u << 21) - 1)) & ~(uintptr_t)((1u << 21) - 1);
     const uintptr_t e = ((uintptr_t)p + n) & ~(uintptr_t)((1u << 21) - 1);
     if (e > a) (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
@@ -437,7 +452,7 @@ int pipeline_d2h(Dev& d, size_t nchunks, size_t chunk_cap, Produce produce, uint
         HIP_TRY(hipStreamWaitEvent(d.cst, d.ev_k[s], 0));
         HIP_TRY(hipMemcpyAsync(d.pin[s].p, dbuf, bytes[s], hipMemcpyDeviceToHost, d.cst));
         HIP_TRY(hipEventRecord(d.ev_c[s], d.cst));
-        if (i == std::min<size_t>(1, nchunks - 1) && out_bytes >= ((size_t)64 << 20))
+        if (i == std::min<size_t>(1, nchunks - 1) && out_bytes >= ((size_t)64 << 20) && prefault_output())
             CopyPool::get().prefault_par(out, out_bytes);   // while the GPU works on chunks 0-1
         if (i >= 1)
             if (int rc = drain(i - 1)) return rc;          // frees pinned slot (i-1)&1 for chunk i+1
@@ -782,23 +797,38 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     return DPF_OK;
 }
 
+// The expanded form's layout depends on (nkeys, stop) (tree_ws), so each
+// expanded workspace is recorded here and dpf_evalfull_expanded_dev refuses
+// one expanded for another shape instead of reading misplaced records.
+std::mutex g_exp_mu;
+std::unordered_map<const void*, std::pair<size_t, uint32_t>>& g_expanded =
+    *new std::unordered_map<const void*, std::pair<size_t, uint32_t>>();
+
 int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN, void* d_work,
                         void* stream) {
     if (int rc = check_key(klen, logN)) return rc;
     DeviceGuard g(device);
     HIP_TRY(expand_keys(d_keys, klen, nkeys, stop_of(logN), tree_ws(d_work, nkeys, stop_of(logN)), (hipStream_t)stream));
+    std::lock_guard<std::mutex> lk(g_exp_mu);
+    g_expanded[d_work] = {nkeys, stop_of(logN)};
     return DPF_OK;
 }
 
-int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
+int dpf_evalfull_expanded_dev(int device, void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
                               uint64_t prefix, uint8_t* d_out, void* stream) {
     if (logN > 63) return fail(DPF_ERR_PARAM, "dpf: logN > 63");
     const uint32_t stop = stop_of(logN);
     if (prefix_bits > stop || (prefix >> prefix_bits) != 0) return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
     if (nkeys == 0) return DPF_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_exp_mu);
+        const auto it = g_expanded.find(d_work);
+        if (it == g_expanded.end() || it->second.first != nkeys || it->second.second != stop)
+            return fail(DPF_ERR_PARAM, "dpf: d_work was not expanded by dpf_expand_keys_dev for this nkeys and logN");
+    }
     DeviceGuard g(device);
     const uint64_t stride = (uint64_t)16 << (stop - prefix_bits);
-    HIP_TRY(run_tree(tree_ws(const_cast<void*>(d_work), nkeys, stop), 0, nkeys, stop, prefix_bits, prefix, d_out, stride,
+    HIP_TRY(run_tree(tree_ws(d_work, nkeys, stop), 0, nkeys, stop, prefix_bits, prefix, d_out, stride,
                      (hipStream_t)stream));
     return DPF_OK;
 }

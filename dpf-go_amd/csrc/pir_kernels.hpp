@@ -1,14 +1,28 @@
-// pir_kernels.hpp — launcher for the PIR answer fold (pir_kernels.hip).
+// pir_kernels.hpp — launcher for the XOR fold (pir_kernels.hip): the PIR
+// answer and the general-payload streaming consumer of EvalFull output.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define DPF_FOLD_PLAN 1   // plan_fold() below (tools/fold_bench.hip)
+
 namespace dpfk {
+
+// How launch_pir_fold covers (rec_bytes, nkeys): `cols` 32-byte columns per
+// pass (1, 2, 4 or 8 = the whole record; 1 with `col_passes` = rec_bytes/32
+// for other widths), `keys_per_pass` keys per DB read, the direct kernel or
+// Four-Russians with `kw` 64-key lane groups sharing each table.
+struct FoldPlan {
+    uint32_t cols, col_passes, keys_per_pass, kw;
+    bool direct;
+};
+FoldPlan plan_fold(uint64_t rec_bytes, uint32_t nkeys);
 
 // ans[k][0 .. rec_bytes) ^= XOR of the records db[i] (rec_bytes each, a
 // multiple of 32; i < nrec) whose bit i is set in bits[k * words_per_key
 // ...] (EvalFull's LSB-first layout).  `parts` is scratch of
-// pir_fold_parts_bytes() (per-workgroup partial answers).
+// pir_fold_parts_bytes() (per-workgroup partial answers).  bits, db 16-byte
+// aligned; words_per_key a multiple of 4 covering nrec bits.
 uint64_t pir_fold_parts_bytes();
 hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const uint8_t* db, uint64_t nrec,
                            uint64_t rec_bytes, uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st);

@@ -94,6 +94,10 @@ int dpf_keys_unpack(const uint8_t* packed, size_t key_len, size_t n, uint8_t* co
  * (dpf.go:206,219), longer keys are accepted.  Shorter: DPF_ERR_KEYLEN. */
 /* Eval (dpf.go:171-211): *out_bit = 0/1. */
 int dpf_eval(const uint8_t* key, size_t key_len, uint64_t x, uint32_t logN, uint8_t* out_bit);
+/* Host output buffers are written by parallel copies from pinned staging;
+ * with DPF_PREFAULT_OUTPUT=1 in the environment, buffers >= 64 MiB also get
+ * a MADV_HUGEPAGE hint and are pre-touched (zeroed) while the GPU works.
+ * Off by default: it changes the caller's memory policy. */
 /* EvalFull (dpf.go:243-262): out = dpf_evalfull_len(logN) bytes. */
 int dpf_evalfull(const uint8_t* key, size_t key_len, uint32_t logN, uint8_t* out);
 /* nkeys x EvalFull; keys packed [nkeys][key_len], out [nkeys][evalfull_len].
@@ -149,11 +153,16 @@ int dpf_aes_mmo_dev(int device, int impl, int right, const uint8_t* d_in, uint8_
 
 /* Two-phase form of the above: expand keys once into d_work (the aligned
  * per-level records the kernels read), then evaluate any number of
- * subtrees from the expanded form.  Lets a caller time the tree kernel
- * alone and reuse expanded keys across calls. */
+ * subtrees of all nkeys keys from the expanded form.  Lets a caller time the
+ * tree kernel alone and reuse expanded keys across calls.  The layout
+ * depends on (nkeys, logN): dpf_evalfull_expanded_dev must pass the nkeys
+ * and logN that dpf_expand_keys_dev used for this d_work, else
+ * DPF_ERR_PARAM.  d_work is also the byte-sliced back end's frontier
+ * scratch, so evaluations from one d_work must not overlap in time (use
+ * one d_work per stream). */
 int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, uint32_t logN, void* d_work,
                         void* stream);
-int dpf_evalfull_expanded_dev(int device, const void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
+int dpf_evalfull_expanded_dev(int device, void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
                               uint64_t prefix, uint8_t* d_out, void* stream);
 
 /* ---- 2-server PIR over a DPF (BASELINE configs[4]; no reference

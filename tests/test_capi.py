@@ -87,6 +87,16 @@ def test_xor_fold_validates_before_touching_a_device():
     assert dpf.xor_fold_workspace_size() > 0
 
 
+def test_expanded_form_requires_an_expanded_workspace():
+    """dpf_evalfull_expanded_dev refuses a d_work that dpf_expand_keys_dev did
+    not expand for this (nkeys, logN): the records' layout depends on both
+    (ADVICE r02).  Checked before any device call."""
+    L = dpf.lib()
+    p = 8192   # fake device address, never dereferenced
+    assert L.dpf_evalfull_expanded_dev(0, p, 4, 20, 0, 0, p, None) == dpf.DPF_ERR_PARAM
+    assert L.dpf_evalfull_expanded_dev(0, p, 0, 20, 0, 0, p, None) == dpf.DPF_OK   # no keys: nothing to do
+
+
 def test_batch_gen_matches_single():
     logN = 20
     al, s0, s1 = synth.key_seeds(64, logN)

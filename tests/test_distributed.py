@@ -97,10 +97,22 @@ def test_bench_gpus_flag_spawns_ranks():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
-                        "--steps", "3", "--warmup", "1"], capture_output=True, text=True, env=env, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
+    def run(*extra):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                            "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.3", *extra],
+                           capture_output=True, text=True, env=env, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        return json.loads(lines[0])
+    d = run()
     assert d["n_gpus"] == 2 and d["dry_run"] and d["local_ranks"] == "2"
+    # N > 1 lines keep the CPU baseline (rank 0, after the timed region) ...
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    # ... and report HBM traffic only where a PMC profile measured that
+    # per-rank shape: a 2-way PIR/split rank runs half a subtree.
+    assert "roofline" in d
+    p = run("--workload", "pir")
+    assert p["roofline"]["traffic"] is None and "traffic_note" in p["roofline"]
+    assert "cpu_baseline" not in p

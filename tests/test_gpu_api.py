@@ -1,0 +1,58 @@
+"""GPU checks of the C-ABI's contracts around the kernels (include/dpf_hip.h):
+the expanded-key form's shape check, and a process that exits without
+dpf_gpu_shutdown (no HIP call from static teardown)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import dpf
+from dpf import synth
+import oracle
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert dpf.gpu_init(1) >= 1
+
+
+def test_expanded_form_checks_nkeys_and_logN():
+    import torch
+    logN, nk = 12, 8
+    al, s0, s1 = synth.key_seeds(nk, logN, first=31)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    kl, olen = dpf.key_len(logN), dpf.evalfull_len(logN)
+    d_keys = torch.from_numpy(ka.reshape(-1)).cuda()
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(nk * olen, dtype=torch.uint8, device="cuda")
+    dpf.expand_keys_dev(d_keys, kl, nk, logN, d_work)
+    for bad_nk, bad_logN in ((nk // 2, logN), (nk, logN + 1)):
+        with pytest.raises(dpf.DPFPanic) as e:
+            dpf.evalfull_expanded_dev(d_work, bad_nk, bad_logN, d_out)
+        assert e.value.code == dpf.DPF_ERR_PARAM
+    dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy().reshape(nk, olen), oracle.evalfull_batch(ka, logN, nthreads=4))
+
+
+def test_process_exits_cleanly_without_shutdown():
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import numpy as np, dpf\n"
+        "from dpf import synth\n"
+        "assert dpf.gpu_init(1) >= 1\n"
+        "al, s0, s1 = synth.key_seeds(4, 14)\n"
+        "ka, kb = dpf.gen_batch_seeded(al, 14, s0, s1)\n"
+        "full = dpf.evalfull_batch(np.concatenate([ka, kb]), 14, ngpus=1)\n"
+        "x = full[:4] ^ full[4:]\n"
+        "assert all(np.unpackbits(x[k], bitorder='little').sum() == 1 for k in range(4))\n"
+        "print('done')\n"   # no dpf_gpu_shutdown: the registry is left to process exit
+    ) % (os.path.join(ROOT, "dpf-go_amd"), os.path.join(ROOT, "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith("done")

@@ -22,7 +22,7 @@ def _keys(nk, logN, first=0):
     return al, ka, kb
 
 
-@pytest.mark.parametrize("logN,nrec,nk", [(7, 128, 3), (10, 1000, 5), (12, 4096, 70), (16, 40000, 9)])
+@pytest.mark.parametrize("logN,nrec,nk", [(7, 128, 3), (10, 1000, 5), (12, 4096, 70), (16, 40000, 9), (12, 4000, 200), (13, 8192, 300)])
 def test_pir_matches_oracle(logN, nrec, nk):
     db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
     _, ka, _ = _keys(nk, logN, first=logN)

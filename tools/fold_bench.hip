@@ -1,10 +1,13 @@
-// fold_bench.hip — isolates the PIR fold kernel at configs[4] shape (2^24
-// records x 32 B, 64 keys, random selection bits laid out as EvalFull
-// writes them) and times it with HIP events.  Build with -DFOLD_SRC=<file>
-// to A/B another revision of pir_kernels.hip (tools/ab/).  One JSON line.
+// fold_bench.hip — isolates the XOR fold (pir_kernels.hip) at configs[4]
+// shape by default (2^24 records x 32 B, 64 keys, random selection bits laid
+// out as EvalFull writes them), times it with HIP events and checks 2 keys'
+// answers against a plain host fold.  Args: [nkeys] [rec_bytes] [log2 nrec].
+// Build with -DFOLD_SRC=<file> to A/B another revision (tools/ab/).  One
+// JSON line.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <vector>
 
 #ifndef FOLD_SRC
@@ -15,39 +18,72 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
 int main(int argc, char** argv) {
-    const uint64_t nrec = 1ull << 24;
     const uint32_t nkeys = argc > 1 ? (uint32_t)atoi(argv[1]) : 64;
+    const uint64_t rec_bytes = argc > 2 ? (uint64_t)atoll(argv[2]) : 32;
+    const uint64_t nrec = argc > 3 ? 1ull << atoi(argv[3]) : 1ull << 24;
     const int iters = 20;
-    const uint64_t wpk = nrec / 32;
+    const uint64_t wpk = (nrec + 127) / 128 * 4;
     void *bits, *db, *ans, *parts;
     CK(hipMalloc(&bits, (size_t)nkeys * wpk * 4));
-    CK(hipMalloc(&db, nrec * 32));
-    CK(hipMalloc(&ans, (size_t)nkeys * 32));
+    CK(hipMalloc(&db, nrec * rec_bytes));
+    CK(hipMalloc(&ans, (size_t)nkeys * rec_bytes));
     CK(hipMalloc(&parts, dpfk::pir_fold_parts_bytes()));
     std::vector<uint32_t> h((size_t)nkeys * wpk);
-    for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)(i * 2654435761u) ^ (uint32_t)(i >> 7);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (auto& v : h) v = (uint32_t)rnd();
+    std::vector<uint8_t> hdb(nrec * rec_bytes);
+    for (size_t i = 0; i < hdb.size(); i += 8) { uint64_t r = rnd(); memcpy(&hdb[i], &r, 8); }
     CK(hipMemcpy(bits, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    CK(hipMemset(db, 0x5a, nrec * 32));
+    CK(hipMemcpy(db, hdb.data(), hdb.size(), hipMemcpyHostToDevice));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int i = 0; i < 3; ++i)
-        CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, 32, nkeys, (uint32_t*)ans,
-                                 (uint32_t*)parts, 0));
+    auto run = [&]() {
+        CK(hipMemsetAsync(ans, 0, (size_t)nkeys * rec_bytes, 0));
+        CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, rec_bytes, nkeys,
+                                 (uint32_t*)ans, (uint32_t*)parts, 0));
+    };
+    // Clock spin-up: an idle MI355X needs a few hundred ms of load to reach
+    // its steady clock.
+    {
+        CK(hipEventRecord(e0, 0));
+        float el = 0;
+        while (el < 400.0f) {
+            for (int i = 0; i < 10; ++i) run();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&el, e0, e1));
+        }
+    }
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < iters; ++i)
-        CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, 32, nkeys, (uint32_t*)ans,
-                                 (uint32_t*)parts, 0));
+    for (int i = 0; i < iters; ++i) run();
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= iters;
-    std::vector<uint32_t> a((size_t)nkeys * 8);
-    CK(hipMemcpy(a.data(), ans, a.size() * 4, hipMemcpyDeviceToHost));
-    uint32_t chk = 0;
-    for (uint32_t v : a) chk = chk * 31 + v;
-    printf("{\"src\": \"%s\", \"nkeys\": %u, \"fold_us\": %.1f, \"GBs\": %.0f, \"check\": %u}\n", FOLD_SRC, nkeys,
-           ms * 1e3, (nrec * 32 + (double)nkeys * wpk * 4) / (ms * 1e-3) / 1e9, chk);
-    return 0;
+    std::vector<uint8_t> a((size_t)nkeys * rec_bytes);
+    CK(hipMemcpy(a.data(), ans, a.size(), hipMemcpyDeviceToHost));
+    int bad = 0;
+    const uint32_t check_keys[2] = {0, nkeys - 1};
+    for (uint32_t k : check_keys) {
+        std::vector<uint8_t> want(rec_bytes, 0);
+        for (uint64_t i = 0; i < nrec; ++i)
+            if ((h[(size_t)k * wpk + i / 32] >> (i % 32)) & 1)
+                for (uint64_t b = 0; b < rec_bytes; ++b) want[b] ^= hdb[i * rec_bytes + b];
+        bad += memcmp(want.data(), &a[(size_t)k * rec_bytes], rec_bytes) != 0;
+    }
+#ifdef DPF_FOLD_PLAN
+    const dpfk::FoldPlan p = dpfk::plan_fold(rec_bytes, nkeys);
+#else
+    struct { uint32_t cols, col_passes, keys_per_pass, kw; bool direct; } p{1, (uint32_t)(rec_bytes / 32), 64, 1, false};
+#endif
+    const double bytes = (double)nrec * rec_bytes + (double)nkeys * nrec / 8;
+    printf("{\"src\": \"%s\", \"nkeys\": %u, \"rec_bytes\": %llu, \"nrec\": %llu, \"kernel\": \"%s\", \"kw\": %u, "
+           "\"col_passes\": %u, \"fold_us\": %.1f, \"GBs\": %.0f, \"db_reads\": %u, \"ok\": %s}\n",
+           FOLD_SRC, nkeys, (unsigned long long)rec_bytes, (unsigned long long)nrec, p.direct ? "direct" : "4r", p.kw,
+           p.col_passes, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
+           p.col_passes * ((nkeys + p.keys_per_pass - 1) / p.keys_per_pass), bad ? "false" : "true");
+    return bad ? 1 : 0;
 }

@@ -21,3 +21,6 @@ for w in eval split pir; do
   rc=$?; echo "bench $w rc=$rc"; grep '^{' "$OUT/bench_$w.log" | tail -1
   [ $rc -eq 0 ] || exit $rc
 done
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -1 "$OUT/smoke.log"
+exit $rc
