@@ -363,7 +363,40 @@ def wl_evalfull(c: Ctx) -> dict:
     line["aes_variants"] = variants
     if c.world == 1 and not a.no_api:
         line["api"] = api_rates(c, ka, logN)
+        line["single_call"] = single_call_latency(c, ka[0].tobytes(), logN)
     return line
+
+
+def single_call_latency(c: Ctx, key: bytes, logN: int) -> dict:
+    """The reference's own call shapes, one key (dpf.go:171 Eval, :243
+    EvalFull), through the drop-in C ABI: the host small-call path
+    (host_eval.cpp, what DPF_SMALL_AUTO picks at this size), the GPU round
+    trip, and the reference-style CPU restatement (oracle, one aes128MMO per
+    call) for scale.  Medians; latency, not throughput."""
+    dpf = c.dpf
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    def med(f, n):
+        f()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    x = 12345 % (1 << logN)
+    prev = dpf.get_small_call_path()
+    out = {"logN": logN, "auto_routes_evalfull_to_host_up_to_logN": dpf.small_call_max_logN()}
+    for mode in ("host", "gpu"):
+        dpf.set_small_call_path(mode)
+        out[f"eval_{mode}_us"] = round(med(lambda: dpf.Eval(key, x, logN), 101) * 1e6, 2)
+        out[f"evalfull_{mode}_ms"] = round(med(lambda: dpf.EvalFull(key, logN), 21) * 1e3, 4)
+    dpf.set_small_call_path(prev)
+    out["eval_ref_style_cpu_us"] = round(med(lambda: oracle.eval_(key, x, logN, aesni=True), 101) * 1e6, 2)
+    out["evalfull_ref_style_cpu_ms"] = round(med(lambda: oracle.evalfull(key, logN, aesni=True), 9) * 1e3, 4)
+    return out
 
 
 def api_rates(c: Ctx, ka: np.ndarray, logN: int, reps: int = 5) -> dict:

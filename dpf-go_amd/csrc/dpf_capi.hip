@@ -241,6 +241,7 @@ class CopyPool {
 // static teardown, whatever the order against the HIP runtime and torch.
 std::mutex g_mu;
 std::vector<std::shared_ptr<Dev>>& g_devs = *new std::vector<std::shared_ptr<Dev>>();
+std::atomic<int> g_ndevs{0};   // g_devs.size(), readable without g_mu (small-call routing)
 
 struct DeviceGuard {
     int prev = -1;
@@ -300,6 +301,7 @@ int open_list(const std::vector<int>& ids) {
         devs.push_back(std::move(d));
     }
     g_devs = std::move(devs);
+    g_ndevs.store((int)g_devs.size());
     return (int)g_devs.size();
 }
 
@@ -646,6 +648,7 @@ void dpf_gpu_shutdown(void) {
     {
         std::lock_guard<std::mutex> lk(g_mu);
         old.swap(g_devs);
+        g_ndevs.store(0);
     }
     // Dropping the registry's references; a device still used by an
     // in-flight call or a PIR handle is released when that lets go.
@@ -697,7 +700,52 @@ int dpf_evalfull_batch(const uint8_t* keys, size_t klen, size_t nkeys, uint32_t 
     });
 }
 
+// ---- small-call path (host_eval.cpp) ------------------------
+std::atomic<int> g_small_mode{[] {
+    const char* e = getenv("DPF_SMALL_CALLS");
+    if (!e) return DPF_SMALL_AUTO;
+    if (e[0] == 'g' || e[0] == 'G') return DPF_SMALL_GPU;
+    if (e[0] == 'h' || e[0] == 'H') return DPF_SMALL_HOST;
+    return DPF_SMALL_AUTO;
+}()};
+
+// Largest logN whose single-key EvalFull goes to the host in AUTO mode: up
+// to it, one key's host EvalFull (3*2^(logN-7) AES on VAES) is faster than
+// the GPU round trip (key H2D, launch, output D2H, sync) -- measured on the
+// GPU box's EPYC (profiles/r03/small_calls).
+constexpr uint32_t kSmallFullMaxLogN = 21;
+
+int dpf_set_small_call_path(int mode) {
+    if (mode != DPF_SMALL_AUTO && mode != DPF_SMALL_GPU && mode != DPF_SMALL_HOST)
+        return fail(DPF_ERR_PARAM, "dpf: unknown small-call mode");
+    return g_small_mode.exchange(mode);
+}
+int dpf_get_small_call_path(void) { return g_small_mode.load(); }
+uint32_t dpf_small_call_max_logN(void) { return kSmallFullMaxLogN; }
+
+// Route a single call to the host?  Only with a gfx950 device open (so the
+// host path is never a stand-in for a missing GPU) and AES-NI present.
+// Returns 1 = host, 0 = GPU, < 0 = error (no device).
+int route_host(bool full, uint32_t logN) {
+    const int mode = g_small_mode.load(std::memory_order_relaxed);
+    if (mode == DPF_SMALL_GPU || !dpfh::host_eval_available()) return 0;
+    if (g_ndevs.load(std::memory_order_acquire) <= 0) {   // open on first use, as the GPU path would
+        int g = 0;
+        (void)pick_devs(1, &g);
+        if (g <= 0) return g;
+    }
+    if (mode == DPF_SMALL_HOST) return 1;
+    return !full || logN <= kSmallFullMaxLogN ? 1 : 0;
+}
+
 int dpf_evalfull(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const int h = route_host(true, logN);
+    if (h < 0) return h;
+    if (h) {
+        dpfh::evalfull_host(key, klen, logN, out);
+        return DPF_OK;
+    }
     return dpf_evalfull_batch(key, klen, 1, logN, out, 1);
 }
 
@@ -715,6 +763,13 @@ int dpf_eval_batch(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_
 }
 
 int dpf_eval(const uint8_t* key, size_t klen, uint64_t x, uint32_t logN, uint8_t* out_bit) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const int h = route_host(false, logN);
+    if (h < 0) return h;
+    if (h) {
+        dpfh::eval_batch_host(key, klen, 1, &x, 1, logN, out_bit);
+        return DPF_OK;
+    }
     return dpf_eval_batch(key, klen, 1, &x, 1, logN, out_bit, 1);
 }
 

@@ -17,4 +17,10 @@ int gen_batch_seeded(const uint64_t* alphas, uint32_t logN, const uint8_t* s0s, 
 int keys_pack(const uint8_t* const* keys, const size_t* lens, size_t n, size_t key_len, uint8_t* out);
 int keys_unpack(const uint8_t* packed, size_t key_len, size_t n, uint8_t* const* keys);
 
+// host_eval.cpp: the single-call path (AES-NI / VAES), bit-exact with the kernels.
+bool host_eval_available();
+void eval_batch_host(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_t* xs, size_t ppk, uint32_t logN,
+                     uint8_t* out);
+void evalfull_host(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out);
+
 }  // namespace dpfh

@@ -79,6 +79,9 @@ SIGNATURES = {
     "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _sz, _vp]),
     "dpf_expand_keys_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp]),
     "dpf_evalfull_expanded_dev": (_int, [_int, _vp, _sz, _u32, _u32, _u64, _vp, _vp]),
+    "dpf_set_small_call_path": (_int, [_int]),
+    "dpf_get_small_call_path": (_int, []),
+    "dpf_small_call_max_logN": (ctypes.c_uint32, []),
     "dpf_set_aes_impl": (_int, [_int]),
     "dpf_get_aes_impl": (_int, []),
     "dpf_aes_mmo_dev": (_int, [_int, _int, _int, _vp, _vp, _sz, _u32, _vp]),
@@ -233,11 +236,27 @@ def gen_batch_seeded(alphas: Sequence[int], logN: int, s0s: np.ndarray, s1s: np.
 
 # ----------------------------------------------------------- evaluation ---
 def Eval(k: bytes, x: int, logN: int) -> int:
-    """dpf.go:171 — the share of f_alpha(x), 0 or 1."""
-    kk = _as_u8(k)
-    out = np.zeros(1, np.uint8)
-    _check(lib().dpf_eval(_buf(kk), kk.size, x & 0xFFFFFFFFFFFFFFFF, logN, _buf(out)))
-    return int(out[0])
+    """dpf.go:171 — the share of f_alpha(x), 0 or 1.  A latency-bound single
+    call: the key bytes go to C without a numpy copy."""
+    kb = k if isinstance(k, bytes) else _as_u8(k).tobytes()
+    out = ctypes.c_uint8(0)
+    rc = _eval_fn()(kb, len(kb), x & 0xFFFFFFFFFFFFFFFF, logN, ctypes.byref(out))
+    if rc != DPF_OK:
+        _check(rc)
+    return out.value
+
+
+_eval_proto = None
+
+
+def _eval_fn():
+    """dpf_eval with a bytes key argument (c_char_p: no copy)."""
+    global _eval_proto
+    if _eval_proto is None:
+        f = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32,
+                             ctypes.POINTER(ctypes.c_uint8))
+        _eval_proto = f(("dpf_eval", lib()))
+    return _eval_proto
 
 
 def EvalFull(key: bytes, logN: int) -> bytes:
@@ -346,6 +365,28 @@ def set_aes_impl(impl) -> int:
 
 def get_aes_impl() -> int:
     return int(lib().dpf_get_aes_impl())
+
+
+SMALL_AUTO, SMALL_GPU, SMALL_HOST = 0, 1, 2
+
+
+def set_small_call_path(mode) -> int:
+    """Route of the single-key Eval/EvalFull ("auto"/"gpu"/"host" or 0/1/2,
+    include/dpf_hip.h); returns the previous mode."""
+    if isinstance(mode, str):
+        mode = {"auto": SMALL_AUTO, "gpu": SMALL_GPU, "host": SMALL_HOST}[mode]
+    rc = lib().dpf_set_small_call_path(mode)
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+def get_small_call_path() -> int:
+    return int(lib().dpf_get_small_call_path())
+
+
+def small_call_max_logN() -> int:
+    return int(lib().dpf_small_call_max_logN())
 
 
 def aes_mmo_dev(d_in, d_out, nblocks: int, impl: int = AES_TTABLE, right: bool = False, reps: int = 1,

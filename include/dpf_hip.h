@@ -145,6 +145,22 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t
 #define DPF_AES_BITSLICED 1
 int dpf_set_aes_impl(int impl);   /* returns the previous back end */
 int dpf_get_aes_impl(void);
+/* ---- small-call path of the single-key API ---------------
+ * dpf_eval and dpf_evalfull are the reference's latency-bound single calls
+ * (dpf.go:171, :243).  DPF_SMALL_AUTO (default) evaluates them on the host's
+ * AES units (host_eval.cpp: AES-NI/VAES, bit-exact with the kernels) when
+ * that beats a GPU round trip: every dpf_eval, and dpf_evalfull up to
+ * logN = dpf_small_call_max_logN(); DPF_SMALL_GPU always uses the GPU,
+ * DPF_SMALL_HOST the host whenever it has AES-NI.  Either way a gfx950
+ * device must be open (DPF_ERR_NODEV otherwise): this is a latency path,
+ * not a fallback.  The batched and _dev entry points always run on the GPU.
+ * Process-wide; default from env DPF_SMALL_CALLS=auto|gpu|host. */
+#define DPF_SMALL_AUTO 0
+#define DPF_SMALL_GPU 1
+#define DPF_SMALL_HOST 2
+int dpf_set_small_call_path(int mode);   /* returns the previous mode */
+int dpf_get_small_call_path(void);
+uint32_t dpf_small_call_max_logN(void);
 /* aes128MMO (aes_amd64.s:51-82) of nblocks (multiple of 8) 16-byte blocks,
  * iterated `reps` times (out = MMO^reps(in)), under the fixed left (right=0)
  * or right key (dpf.go:23-24): the AES blocks/s microbenchmark + self-test. */

@@ -19,6 +19,9 @@ NT = 16
 @pytest.fixture(scope="module", autouse=True)
 def _gpu():
     assert dpf.gpu_init(1) >= 1
+    prev = dpf.set_small_call_path("gpu")      # single-key calls here check the kernels
+    yield
+    dpf.set_small_call_path(prev)
 
 
 def _keys(nk, logN, first=0):

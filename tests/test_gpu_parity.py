@@ -22,7 +22,12 @@ NT = 16
 def _gpu():
     n = dpf.gpu_init(1)
     assert n >= 1
+    # The single-key dpf.Eval / dpf.EvalFull calls here are GPU parity checks:
+    # pin them to the kernels (auto mode would route small ones to the host
+    # path, which tests/test_gpu_small_calls.py covers).
+    prev = dpf.set_small_call_path("gpu")
     yield
+    dpf.set_small_call_path(prev)
 
 
 def _bits(a: np.ndarray) -> np.ndarray:

@@ -1,0 +1,75 @@
+"""The single-key API's small-call path (include/dpf_hip.h
+DPF_SMALL_*): dpf_eval / dpf_evalfull on the host's AES units when that
+beats a GPU round trip.  Bit-exact with the oracle (dpf.go:171-262) in every
+mode, routed as documented, and never without an open GPU."""
+import time
+
+import numpy as np
+import pytest
+
+import dpf
+from dpf import synth
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert dpf.gpu_init(1) >= 1
+    prev = dpf.get_small_call_path()
+    yield
+    dpf.set_small_call_path(prev)
+
+
+@pytest.mark.parametrize("mode", ["host", "auto", "gpu"])
+@pytest.mark.parametrize("logN", [3, 7, 12, 20, 22])
+def test_single_calls_match_oracle(mode, logN):
+    dpf.set_small_call_path(mode)
+    al, s0, s1 = synth.key_seeds(2, logN, first=5000 + logN)
+    ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+    for k in (ka[0], kb[1]):
+        assert dpf.EvalFull(k.tobytes(), logN) == oracle.evalfull(k.tobytes(), logN, aesni=True)
+        for x in list(synth.eval_points(1, 6, logN)[0]) + [int(al[0]), (1 << 63) | 5]:
+            assert dpf.Eval(k.tobytes(), int(x), logN) == oracle.eval_(k.tobytes(), int(x), logN, aesni=True)
+
+
+def test_two_server_property_through_the_host_path():
+    dpf.set_small_call_path("host")
+    logN = 16
+    al, s0, s1 = synth.key_seeds(3, logN, first=61)
+    ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+    for j in range(3):
+        x = np.frombuffer(dpf.EvalFull(ka[j].tobytes(), logN), np.uint8) ^ \
+            np.frombuffer(dpf.EvalFull(kb[j].tobytes(), logN), np.uint8)
+        bits = np.unpackbits(x, bitorder="little")
+        assert bits.sum() == 1 and bits[int(al[j])] == 1
+
+
+def test_short_key_still_panics_like_the_reference():
+    dpf.set_small_call_path("host")
+    with pytest.raises(dpf.DPFPanic) as e:
+        dpf.EvalFull(bytes(40), 20)
+    assert e.value.code == dpf.DPF_ERR_KEYLEN
+
+
+def test_auto_mode_is_faster_than_the_gpu_round_trip_where_it_routes():
+    """Sanity of the threshold: at logN = small_call_max_logN() and below,
+    the host call is not slower than the GPU call (median of 15)."""
+    logN = dpf.small_call_max_logN()
+    al, s0, s1 = synth.key_seeds(1, logN, first=9)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    key = ka[0].tobytes()
+
+    def med(mode):
+        dpf.set_small_call_path(mode)
+        dpf.EvalFull(key, logN)
+        ts = []
+        for _ in range(15):
+            t0 = time.perf_counter()
+            dpf.EvalFull(key, logN)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    host, gpu = med("host"), med("gpu")
+    assert host <= gpu * 1.25, (host, gpu)
