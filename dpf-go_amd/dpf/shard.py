@@ -44,13 +44,42 @@ def xor_fold(parts: np.ndarray) -> np.ndarray:
 
 
 def gather_xor(partial, group=None) -> np.ndarray:
-    """All-gather every rank's uint8 partial answer tensor and XOR them on the
-    host.  Works for the nccl (RCCL) and gloo backends."""
+    """All-gather every rank's uint8 partial answer tensor and XOR them.
+    RCCL (nccl backend) has no XOR reduction: the partials are gathered into
+    one [world, ...] device tensor, XOR-combined on the device (world - 1
+    elementwise XORs over 64-bit words) and copied to the host once.  gloo
+    (CPU rehearsals and tests) gathers host tensors and XORs with numpy."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    if dist.get_backend(group) == "gloo" and partial.is_cuda:
-        partial = partial.cpu()
-    bufs = [torch.empty_like(partial) for _ in range(world)]
-    dist.all_gather(bufs, partial, group=group)
-    return xor_fold(np.stack([b.cpu().numpy() for b in bufs]))
+    if dist.get_backend(group) == "gloo":
+        if partial.is_cuda:
+            partial = partial.cpu()
+        bufs = [torch.empty_like(partial) for _ in range(world)]
+        dist.all_gather(bufs, partial, group=group)
+        return xor_fold(np.stack([b.numpy() for b in bufs]))
+    part = partial.contiguous()
+    out = torch.empty((world,) + tuple(part.shape), dtype=part.dtype, device=part.device)
+    dist.all_gather_into_tensor(out, part, group=group)
+    return xor_rows(out).cpu().numpy()
+
+
+def xor_rows(t):
+    """XOR of t[0], t[1], ... (a uint8 torch tensor [world, ...]) on t's
+    device, 8 bytes per lane when the row length allows."""
+    world = t.shape[0]
+    flat = t.reshape(world, -1)
+    wide = flat.shape[1] % 8 == 0
+    if wide:
+        flat = flat.view(torch_int64())
+    acc = flat[0].clone()
+    for r in range(1, world):
+        acc.bitwise_xor_(flat[r])
+    if wide:
+        acc = acc.view(t.dtype)
+    return acc.view(t.shape[1:])
+
+
+def torch_int64():
+    import torch
+    return torch.int64

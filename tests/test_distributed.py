@@ -116,3 +116,15 @@ def test_bench_gpus_flag_spawns_ranks():
     p = run("--workload", "pir")
     assert p["roofline"]["traffic"] is None and "traffic_note" in p["roofline"]
     assert "cpu_baseline" not in p
+
+
+def test_xor_rows_matches_numpy():
+    """The device-side combine of the RCCL gather (shard.gather_xor), checked
+    on CPU tensors: 8-byte lanes and the byte fallback."""
+    import torch
+    rng = np.random.default_rng(5)
+    for shape in ((8, 64, 32), (2, 5, 3), (1, 16)):
+        a = rng.integers(0, 256, shape, dtype=np.uint8)
+        got = shard.xor_rows(torch.from_numpy(a)).numpy()
+        assert got.shape == a.shape[1:]
+        assert np.array_equal(got, shard.xor_fold(a))
