@@ -121,6 +121,36 @@ hipError_t launch_unpack_both(const uint8_t* keys, uint64_t key_len, uint64_t nk
     return hipGetLastError();
 }
 
+// The byte-sliced records from the T-table records already in the
+// workspace (ek, k_unpack's layout: 16 CW bytes as 4 little-endian words,
+// then tLCW, tRCW as words 4, 5), one thread per output word.  Lets the
+// T-table paths unpack only their own 8-word records and build these only
+// when the byte-sliced back end runs.
+__global__ void k_bs_from_ek(const uint32_t* __restrict__ ek, uint64_t nkeys, uint32_t stop,
+                             uint32_t* __restrict__ ekb) {
+    const uint64_t per = bs_key_words(stop);
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nkeys * per) return;
+    const uint64_t k = i / per, rem = i % per;
+    const uint32_t rb = (uint32_t)(rem / kBsRec), j = (uint32_t)(rem % kBsRec);   // rb == stop: the final CW
+    const uint32_t* rec = ek + k * ((uint64_t)(stop + 2) * 8) + (uint64_t)(rb + 1) * 8;
+    uint32_t v;
+    if (j < 32) {
+        v = planes_word(reinterpret_cast<const uint8_t*>(rec), j >> 3, j & 7);
+    } else {
+        const uint8_t t = (uint8_t)rec[4 + ((j - 32) >> 1)];   // tLCW for 32/33, tRCW for 34/35
+        v = (j & 1) ? (t > 1 ? ~0u : 0u) : (t == 1 ? ~0u : 0u);
+    }
+    ekb[i] = v;
+}
+
+hipError_t launch_bs_from_ek(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t* ekb, hipStream_t st) {
+    const uint64_t n = nkeys * bs_key_words(stop);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bs_from_ek, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, ek, nkeys, stop, ekb);
+    return hipGetLastError();
+}
+
 // Child set after aes_mmo8 (o = MMO(x)): split the control bits off (byte 0
 // of row 0 / plane 0), clear them, apply the parent's correction (dpf.go:
 // 61-68,230-238).  tp: parent "t != 0" mask (bit i of every byte = block i).

@@ -46,6 +46,8 @@ uint32_t bs_depth(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits);
 uint64_t bs_frontier_bytes(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits);
 
 // T-table records (ek, k_unpack's layout) and byte-sliced records (ekb) in one launch.
+// Byte-sliced records from the T-table records (ek) already in a workspace.
+hipError_t launch_bs_from_ek(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t* ekb, hipStream_t st);
 hipError_t launch_unpack_both(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ek,
                               uint32_t* ekb, hipStream_t st);
 hipError_t launch_unpack_bs(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ekb,

@@ -376,15 +376,22 @@ TreeWs tree_ws(void* work, size_t nk, uint32_t stop) {
     return w;
 }
 
-// Key records for both back ends (the byte-sliced words are 3% of a tree launch at configs[1]).
-hipError_t expand_keys(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t stop, const TreeWs& w, hipStream_t st) {
-    return dpfk::launch_unpack_both(d_keys, klen, nk, stop, w.ek, w.ekb, st);
+// The back end a call uses, decided once per call (expansion and launches agree).
+bool want_bs() { return g_aes_impl.load(std::memory_order_relaxed) == DPF_AES_BITSLICED; }
+
+// Key records: the T-table's 8-word records always; the byte-sliced planes
+// (7.6 MB at configs[1], 2/3 of the unpack time) only for the byte-sliced back end.
+hipError_t expand_keys(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t stop, const TreeWs& w, hipStream_t st,
+                       bool bs) {
+    if (bs) return dpfk::launch_unpack_both(d_keys, klen, nk, stop, w.ek, w.ekb, st);
+    return dpfk::launch_unpack(d_keys, klen, nk, stop, w.ek, st);
 }
 
-// Leaves of subtree (prefix_bits, prefix) of keys [k0, k0 + n) through the selected back end.
+// Leaves of subtree (prefix_bits, prefix) of keys [k0, k0 + n): byte-sliced
+// when bs (its records expanded) and the subtree is deep enough, else T-table.
 hipError_t run_tree(const TreeWs& w, size_t k0, size_t n, uint32_t stop, uint32_t prefix_bits, uint64_t prefix,
-                    uint8_t* out, uint64_t stride, hipStream_t st) {
-    if (g_aes_impl.load(std::memory_order_relaxed) == DPF_AES_BITSLICED && dpfk::bs_applicable(stop, prefix_bits))
+                    uint8_t* out, uint64_t stride, hipStream_t st, bool bs) {
+    if (bs && dpfk::bs_applicable(stop, prefix_bits))
         return dpfk::launch_evalfull_bs(w.ek + k0 * dpfk::ek_words(stop), w.ekb + k0 * dpfk::bs_key_words(stop), n, stop,
                                         prefix_bits, prefix, out, stride, w.frontier, st);
     return dpfk::launch_evalfull(w.ek + k0 * dpfk::ek_words(stop), n, stop, prefix_bits, prefix, out, stride, st);
@@ -474,12 +481,13 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
     HIP_TRY(hipError_t(d.work.ensure(tree_ws_bytes(nk, stop, 0, std::min(per, nk)))));
     HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
     const TreeWs w = tree_ws(d.work.p, nk, stop);
-    HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, nk, stop, w, d.st));
+    const bool bs = want_bs();
+    HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, nk, stop, w, d.st, bs));
     if (olen <= kStageBytes) {
         const size_t nch = (nk + per - 1) / per;
         return pipeline_d2h(d, nch, std::min(per, nk) * olen, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
             const size_t k0 = i * per, n = std::min(per, nk - k0);
-            HIP_TRY(run_tree(w, k0, n, stop, 0, 0, dbuf, olen, d.st));
+            HIP_TRY(run_tree(w, k0, n, stop, 0, 0, dbuf, olen, d.st, bs));
             bytes = n * olen;
             off = k0 * olen;
             return DPF_OK;
@@ -490,7 +498,7 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
     const size_t slab = olen >> pb, per_key = (size_t)1 << pb;
     return pipeline_d2h(d, nk * per_key, slab, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
         const size_t k = i / per_key, p = i % per_key;
-        HIP_TRY(run_tree(w, k, 1, stop, pb, p, dbuf, slab, d.st));
+        HIP_TRY(run_tree(w, k, 1, stop, pb, p, dbuf, slab, d.st, bs));
         bytes = slab;
         off = k * olen + p * slab;
         return DPF_OK;
@@ -794,13 +802,14 @@ int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* 
         HIP_TRY(hipError_t(d.work.ensure(tree_ws_bytes(1, stop, pb, 1))));
         HIP_TRY(hipMemcpyAsync(d.keys.p, key, klen, hipMemcpyHostToDevice, d.st));
         const TreeWs w = tree_ws(d.work.p, 1, stop);
-        HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, 1, stop, w, d.st));
+        const bool bs = want_bs();
+        HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, 1, stop, w, d.st, bs));
         // This device's subtree (pb, lo), streamed out in sub-slabs (pb + extra, lo * 2^extra + j).
         uint32_t extra = 0;
         while ((slab >> extra) > kStageBytes && pb + extra < stop) ++extra;
         const size_t sub = slab >> extra;
         return pipeline_d2h(d, (size_t)1 << extra, sub, [&](size_t j, uint8_t* dbuf, size_t& bytes, size_t& off) {
-            HIP_TRY(run_tree(w, 0, 1, stop, pb + extra, ((uint64_t)lo << extra) + j, dbuf, sub, d.st));
+            HIP_TRY(run_tree(w, 0, 1, stop, pb + extra, ((uint64_t)lo << extra) + j, dbuf, sub, d.st, bs));
             bytes = sub;
             off = lo * slab + j * sub;
             return DPF_OK;
@@ -817,9 +826,10 @@ int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t klen, siz
     if (nkeys == 0) return DPF_OK;
     DeviceGuard g(device);
     const TreeWs w = tree_ws(d_work, nkeys, stop);
-    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, (hipStream_t)stream));
+    const bool bs = want_bs();
+    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, (hipStream_t)stream, bs));
     HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, d_out, (uint64_t)16 << (stop - prefix_bits),
-                     (hipStream_t)stream));
+                     (hipStream_t)stream, bs));
     return DPF_OK;
 }
 
@@ -856,16 +866,25 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
 // expanded workspace is recorded here and dpf_evalfull_expanded_dev refuses
 // one expanded for another shape instead of reading misplaced records.
 std::mutex g_exp_mu;
-std::unordered_map<const void*, std::pair<size_t, uint32_t>>& g_expanded =
-    *new std::unordered_map<const void*, std::pair<size_t, uint32_t>>();
+// Also records whether the byte-sliced planes were built: the T-table back
+// end expands only its own records, and switching to the byte-sliced one
+// later derives them from those (launch_bs_from_ek) on first use.
+struct Expanded {
+    size_t nkeys;
+    uint32_t stop;
+    bool bs;
+};
+std::unordered_map<const void*, Expanded>& g_expanded = *new std::unordered_map<const void*, Expanded>();
 
 int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN, void* d_work,
                         void* stream) {
     if (int rc = check_key(klen, logN)) return rc;
     DeviceGuard g(device);
-    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop_of(logN), tree_ws(d_work, nkeys, stop_of(logN)), (hipStream_t)stream));
+    const bool bs = want_bs();
+    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop_of(logN), tree_ws(d_work, nkeys, stop_of(logN)), (hipStream_t)stream,
+                        bs));
     std::lock_guard<std::mutex> lk(g_exp_mu);
-    g_expanded[d_work] = {nkeys, stop_of(logN)};
+    g_expanded[d_work] = {nkeys, stop_of(logN), bs};
     return DPF_OK;
 }
 
@@ -875,16 +894,21 @@ int dpf_evalfull_expanded_dev(int device, void* d_work, size_t nkeys, uint32_t l
     const uint32_t stop = stop_of(logN);
     if (prefix_bits > stop || (prefix >> prefix_bits) != 0) return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
     if (nkeys == 0) return DPF_OK;
+    const bool bs = want_bs();
+    bool build_bs = false;
     {
         std::lock_guard<std::mutex> lk(g_exp_mu);
         const auto it = g_expanded.find(d_work);
-        if (it == g_expanded.end() || it->second.first != nkeys || it->second.second != stop)
+        if (it == g_expanded.end() || it->second.nkeys != nkeys || it->second.stop != stop)
             return fail(DPF_ERR_PARAM, "dpf: d_work was not expanded by dpf_expand_keys_dev for this nkeys and logN");
+        build_bs = bs && !it->second.bs;
+        if (build_bs) it->second.bs = true;
     }
     DeviceGuard g(device);
+    const TreeWs w = tree_ws(d_work, nkeys, stop);
+    if (build_bs) HIP_TRY(dpfk::launch_bs_from_ek(w.ek, nkeys, stop, w.ekb, (hipStream_t)stream));
     const uint64_t stride = (uint64_t)16 << (stop - prefix_bits);
-    HIP_TRY(run_tree(tree_ws(d_work, nkeys, stop), 0, nkeys, stop, prefix_bits, prefix, d_out, stride,
-                     (hipStream_t)stream));
+    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, d_out, stride, (hipStream_t)stream, bs));
     return DPF_OK;
 }
 
@@ -913,8 +937,9 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     const TreeWs w = tree_ws(d_work, nkeys, stop);
     uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
     const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
-    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st));
-    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st));
+    const bool bs = want_bs();
+    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st, bs));
+    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st, bs));
     uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
     HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, 32, (uint32_t)nkeys, (uint32_t*)d_ans,
                                   parts, st));

@@ -56,3 +56,28 @@ def test_process_exits_cleanly_without_shutdown():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().endswith("done")
+
+
+def test_expanded_form_builds_byte_sliced_records_on_first_use():
+    """Expanded under the T-table back end (8-word records only), evaluated
+    under the byte-sliced one: its records are derived from the expanded
+    T-table records (launch_bs_from_ek) on first use, bit-exact."""
+    import torch
+    logN, nk = 16, 12
+    al, s0, s1 = synth.key_seeds(nk, logN, first=88)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    kl, olen = dpf.key_len(logN), dpf.evalfull_len(logN)
+    d_keys = torch.from_numpy(ka.reshape(-1)).cuda()
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device="cuda")
+    want = oracle.evalfull_batch(ka, logN, nthreads=4)
+    prev = dpf.set_aes_impl("ttable")
+    try:
+        dpf.expand_keys_dev(d_keys, kl, nk, logN, d_work)
+        dpf.set_aes_impl("bitsliced")
+        for _ in range(2):    # first use builds the planes, the second reuses them
+            d_out = torch.zeros(nk * olen, dtype=torch.uint8, device="cuda")
+            dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)
+            torch.cuda.synchronize()
+            assert np.array_equal(d_out.cpu().numpy().reshape(nk, olen), want)
+    finally:
+        dpf.set_aes_impl(prev)
