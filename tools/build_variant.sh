@@ -19,5 +19,5 @@ for f in dpf_kernels bs_kernels pir_kernels dpf_capi; do
 done
 wait
 $HIPCC --offload-arch=gfx950 -shared -fPIC -o "$L/variants/libdpf_hip_$NAME.so" \
-    "$O/dpf_kernels.o" "$O/bs_kernels.o" "$O/pir_kernels.o" "$O/dpf_capi.o" "$L/host_gen.o" -lpthread
+    "$O/dpf_kernels.o" "$O/bs_kernels.o" "$O/pir_kernels.o" "$O/dpf_capi.o" "$L/host_gen.o" "$L/host_eval.o" -lpthread
 echo "$L/variants/libdpf_hip_$NAME.so"

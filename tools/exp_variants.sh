@@ -8,7 +8,7 @@ cd "$REPO"
 OUT="gpurun_out/$1"; shift
 mkdir -p "$OUT"
 B=(--steps 50 --warmup 10 --spinup 0.5 --no-cpu-baseline --no-variants --no-api --aes ttable)
-lib() { if [ "$1" = base ]; then echo "$REPO/dpf-go_amd/lib/libdpf_hip.so"; else echo "$REPO/dpf-go_amd/lib/variants/libdpf_hip_$1.so"; fi; }
+lib() { if [ "$1" = base ]; then echo "$REPO/dpf-go_amd/lib/libdpf_hip.so"; elif [ -f "$REPO/tools/bin/libdpf_hip_$1.so" ]; then echo "$REPO/tools/bin/libdpf_hip_$1.so"; else echo "$REPO/dpf-go_amd/lib/variants/libdpf_hip_$1.so"; fi; }
 for r in 1 2; do
   for v in "$@"; do
     DPF_LIB=$(lib $v) timeout -k 10 200 python bench.py "${B[@]}" --check > "$OUT/${v}_$r.log" 2>&1 || { echo "FAIL $v"; tail -5 "$OUT/${v}_$r.log"; exit 1; }
