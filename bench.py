@@ -308,10 +308,17 @@ def wl_evalfull(c: Ctx) -> dict:
     the default); the other back end is timed the same way right after and
     reported under "aes_variants" (configs[1]: bitsliced vs LDS T-table)."""
     a, dpf, torch = c.args, c.dpf, c.torch
-    from dpf import synth
-    logN, nk = a.logN, a.nkeys
+    from dpf import synth, shard
+    logN = a.logN
+    if a.strong:
+        # SURVEY 8d's strong-scaling form: a fixed batch of a.nkeys keys split
+        # over the ranks by range (no collective).
+        lo, hi = shard.key_range(a.nkeys, c.world, c.rank)
+        nk, first = hi - lo, lo
+    else:
+        nk, first = a.nkeys, c.rank * a.nkeys                        # weak: this rank's own batch
     kl, olen = dpf.key_len(logN), dpf.evalfull_len(logN)
-    al, s0, s1 = synth.key_seeds(nk, logN, first=c.rank * nk)      # this rank's own keys
+    al, s0, s1 = synth.key_seeds(nk, logN, first=first)
     ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
     d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
     d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=c.dev)
@@ -349,17 +356,20 @@ def wl_evalfull(c: Ctx) -> dict:
                                   "aes_blocks_per_s": aes / (k2 * 1e-3),
                                   "points_per_s": nk * (1 << logN) / (t2 / max(5, a.steps // 2)),
                                   "bit_identical_first_64_keys": bool(torch.equal(ref, d_out.view(nk, olen)[:64]))}
-    line = c.line(metric=METRIC, value=nk * (1 << logN) * c.world / sec, unit="points/s",
-                  ms_per_step=sec * 1e3, scaling="weak",
+    total = a.nkeys if a.strong else nk * c.world
+    line = c.line(metric=METRIC, value=total * (1 << logN) / sec, unit="points/s",
+                  ms_per_step=sec * 1e3, scaling="strong" if a.strong else "weak",
                   data="synthetic (SplitMix64 seed 0x5EEDD9F0 keys via host Gen)",
-                  config={"workload": f"batched EvalFull, {nk} keys x logN={logN} per GPU (BASELINE configs[1])",
+                  config={"workload": (f"batched EvalFull, {a.nkeys} keys x logN={logN} split over {c.world} GPU(s)"
+                                       if a.strong else
+                                       f"batched EvalFull, {nk} keys x logN={logN} per GPU") + " (BASELINE configs[1])",
                           "keys_per_gpu": nk, "logN": logN, "aes": names[main_impl],
                           "parallelism": f"key-shard x{c.world}"},
-                  aes_blocks_per_s=aes * c.world / sec)
+                  aes_blocks_per_s=total * aes_full(logN) / sec)
     kern = (f"k_evalfull<{min(stop_of(logN), 7)}, true, false>" if main_impl == dpf.AES_TTABLE
             else "k_evalfull<NODES>+k_evalfull_bs<true>")
     line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), kern, k_ms, nk * olen + nk * (stop_of(logN) + 2) * 32,
-                                    aes_impl=names[main_impl])
+                                    aes_impl=names[main_impl], profiled_shape=(nk == 4096))
     line["aes_variants"] = variants
     if c.world == 1 and not a.no_api:
         line["api"] = api_rates(c, ka, logN)
@@ -703,6 +713,8 @@ def main() -> None:
     ap.add_argument("--no-variants", action="store_true", help="skip timing the other AES back end")
     ap.add_argument("--no-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) API rates")
     ap.add_argument("--no-sweep", action="store_true", help="pir: skip the B in {1,16,64,256} batch sweep")
+    ap.add_argument("--strong", action="store_true",
+                    help="evalfull: split a fixed --nkeys over the ranks (strong scaling) instead of --nkeys per rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--spinup", type=float, default=0.5,
                     help="seconds of untimed steps before the warmup (GPU clock ramp); 0 disables")
