@@ -177,3 +177,22 @@ func (p *PirDB) Close() {
 		p.h = nil
 	}
 }
+
+// Small-call routing of the single-key Eval / EvalFull (include/dpf_hip.h
+// DPF_SMALL_*): SmallAuto (default) evaluates them on the host's AES units
+// when that beats a GPU round trip, SmallGPU always uses the GPU, SmallHost
+// the host whenever it has AES-NI.  A gfx950 device must be present in every
+// mode.  Returns the previous mode.
+const (
+	SmallAuto = 0
+	SmallGPU  = 1
+	SmallHost = 2
+)
+
+func SetSmallCallPath(mode int) int {
+	rc := C.dpf_set_small_call_path(C.int(mode))
+	if rc < 0 {
+		check(rc)
+	}
+	return int(rc)
+}
