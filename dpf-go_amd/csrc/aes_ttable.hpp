@@ -120,6 +120,35 @@ __device__ __forceinline__ void aes_last(const uint8_t* tab, uint32_t lo, const 
     s.c0 = n0; s.c1 = n1; s.c2 = n2; s.c3 = n3;
 }
 
+// A round as two phases: the 16 lookups of a block issued together, then
+// its 4 columns.  aes2_rounds<BATCH = true> issues both blocks' 32 lookups
+// before any XOR, with scheduling fences between the phases, so a wave keeps
+// up to 32 LDS reads in flight; left alone the compiler consumes them in
+// groups of 4-8 (r03: 95.7-96.1 vs 93.1-93.4 G blocks/s in the configs[1]
+// tree kernel).  Needs ~16 more VGPRs: the tree kernels use it where they
+// fit (one key per wave) and the interleaved form elsewhere.
+template <int C0 = 0, int C1 = 4>
+__device__ __forceinline__ void round_loads(const uint8_t* tab, uint32_t lo, const Blk& s, uint32_t (&t)[16]) {
+    const uint32_t c[4] = {s.c0, s.c1, s.c2, s.c3};
+#pragma unroll
+    for (int j = C0; j < C1; ++j) {
+        t[4 * j + 0] = tl<0>(tab, c[j], lo);
+        t[4 * j + 1] = tl<1, true>(tab, c[(j + 1) & 3], lo);
+        t[4 * j + 2] = tl<2>(tab, c[(j + 2) & 3], lo);
+        t[4 * j + 3] = tl<3, true>(tab, c[(j + 3) & 3], lo);
+    }
+}
+template <int R, class K>
+__device__ __forceinline__ void round_mix(const K& k, const uint32_t (&t)[16], Blk& s) {
+    auto col = [&](int j, uint32_t rk16) {
+        return xor3(t[4 * j], t[4 * j + 1], rotl(xor3(t[4 * j + 2], t[4 * j + 3], rk16), 16));
+    };
+    s.c0 = col(0, k.template get16<4 * R + 0>());
+    s.c1 = col(1, k.template get16<4 * R + 1>());
+    s.c2 = col(2, k.template get16<4 * R + 2>());
+    s.c3 = col(3, k.template get16<4 * R + 3>());
+}
+
 template <int R, class K>
 __device__ __forceinline__ void aes_rounds(const uint8_t* tab, uint32_t lo, const K& k, Blk& s) {
     if constexpr (R <= 9) {
@@ -129,13 +158,23 @@ __device__ __forceinline__ void aes_rounds(const uint8_t* tab, uint32_t lo, cons
 }
 
 // Two independent AES-MMO blocks, rounds interleaved for ILP.
-template <int R, class KA, class KB>
+template <int R, bool BATCH, class KA, class KB>
 __device__ __forceinline__ void aes2_rounds(const uint8_t* tab, uint32_t lo, const KA& ka, Blk& a, const KB& kb,
                                             Blk& b) {
     if constexpr (R <= 9) {
-        aes_round<R>(tab, lo, ka, a);
-        aes_round<R>(tab, lo, kb, b);
-        aes2_rounds<R + 1>(tab, lo, ka, a, kb, b);
+        if constexpr (BATCH) {
+            uint32_t ta[16], tb[16];
+            round_loads(tab, lo, a, ta);
+            round_loads(tab, lo, b, tb);
+            __builtin_amdgcn_sched_barrier(0);
+            round_mix<R>(ka, ta, a);
+            round_mix<R>(kb, tb, b);
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            aes_round<R>(tab, lo, ka, a);
+            aes_round<R>(tab, lo, kb, b);
+        }
+        aes2_rounds<R + 1, BATCH>(tab, lo, ka, a, kb, b);
     }
 }
 
@@ -151,12 +190,12 @@ __device__ __forceinline__ Blk mmo1(const uint8_t* tab, uint32_t lo, const K& k,
     return bxor(s, x);
 }
 
-template <class KA, class KB>
+template <bool BATCH = false, class KA, class KB>
 __device__ __forceinline__ void mmo2(const uint8_t* tab, uint32_t lo, const KA& ka, Blk xa, Blk& oa, const KB& kb,
                                      Blk xb, Blk& ob) {
     Blk a = bxor(xa, bkey4(ka.template get<0>(), ka.template get<1>(), ka.template get<2>(), ka.template get<3>()));
     Blk b = bxor(xb, bkey4(kb.template get<0>(), kb.template get<1>(), kb.template get<2>(), kb.template get<3>()));
-    aes2_rounds<1>(tab, lo, ka, a, kb, b);
+    aes2_rounds<1, BATCH>(tab, lo, ka, a, kb, b);
     aes_last(tab, lo, ka, a);
     aes_last(tab, lo, kb, b);
     oa = bxor(a, xa);

@@ -64,20 +64,21 @@ __device__ __forceinline__ Blk load_blk(const uint32_t* p) {
 // software pipeline (each block's 16 lookups issued while the other block's
 // are in flight, up to 32 per wave) was slower again: 93.1 vs 93.8 in-tree,
 // 21 VGPRs spilled (profiles/r02/pipe).
-template <class KA, class KB>
+template <bool B = false, class KA, class KB>
 __device__ __forceinline__ void mmo_pair(const uint8_t* tab, uint32_t lo, const KA& ka, Blk xa, Blk& oa,
                                          const KB& kb, Blk xb, Blk& ob) {
 #if DPF_MMO_INTERLEAVE
-    mmo2(tab, lo, ka, xa, oa, kb, xb, ob);
+    mmo2<B>(tab, lo, ka, xa, oa, kb, xb, ob);
 #else
     oa = mmo1(tab, lo, ka, xa);
     ob = mmo1(tab, lo, kb, xb);
 #endif
 }
 
+template <bool B = false>
 __device__ __forceinline__ void expand(const uint8_t* tab, uint32_t lo, const Node& n, const CW& cw, Node& L,
                                        Node& R) {
-    mmo_pair(tab, lo, KeyFixed<false>{}, n.s, L.s, KeyFixed<true>{}, n.s, R.s);
+    mmo_pair<B>(tab, lo, KeyFixed<false>{}, n.s, L.s, KeyFixed<true>{}, n.s, R.s);
     uint32_t tL = L.s.c0 & 1u, tR = R.s.c0 & 1u;
     L.s.c0 &= ~1u;
     R.s.c0 &= ~1u;
@@ -148,19 +149,24 @@ __device__ __forceinline__ Blk bsel(bool b, const Blk& x, const Blk& y) {
 // two inlined copies: the tree kernel's innermost loop must fit the
 // instruction cache (64 KiB per two CUs).  Fully inlined, the PAIR path's
 // loop body was ~85 KiB of code (22 AES-MMO bodies).
+template <bool B>
 __device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& n, uint8_t* p) {
     CW cw = load_cw(c.ek, lvl);
     Node L, R;
-    expand(c.tab, c.lo, n, cw, L, R);
+    expand<B>(c.tab, c.lo, n, cw, L, R);
     CW cw1 = load_cw(c.ek, lvl + 1);
     Blk o0 = {}, o1 = {}, o2, o3;
+    // Only the pending child stays live through the first iteration (a
+    // select of L or R at the top of each iteration kept both live: 5 more
+    // VGPRs at every level of the expansion).
+    Node m = L;
+    const Node pend = R;
 #pragma nounroll
     for (int h = 0; h < 2; ++h) {
-        const Node m = sel(h == 0, L, R);
         Node a, b;
-        expand(c.tab, c.lo, m, cw1, a, b);
+        expand<B>(c.tab, c.lo, m, cw1, a, b);
         Blk oa, ob;
-        mmo_pair(c.tab, c.lo, KeyFixed<false>{}, a.s, oa, KeyFixed<false>{}, b.s, ob);
+        mmo_pair<B>(c.tab, c.lo, KeyFixed<false>{}, a.s, oa, KeyFixed<false>{}, b.s, ob);
         oa = leaf_fix(oa, a.t, c.fcw);
         ob = leaf_fix(ob, b.t, c.fcw);
         o2 = oa;
@@ -169,6 +175,7 @@ __device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& 
             o0 = oa;
             o1 = ob;
         }
+        m = pend;
     }
     store16(p, o0);
     store16(p + 16, o1);
@@ -181,7 +188,9 @@ __device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& 
 // registers while the left subtree is expanded.  Leaf mode writes the
 // converted leaves (dpf.go:214-224); node mode (NODES) writes the 2^D nodes
 // D levels down instead: the frontier a batched Eval continues from.
-template <int DMAX, int D, bool NODES, bool PAIR>
+// B: batched AES rounds (aes_ttable.hpp aes2_rounds) where the registers
+// allow it: the one-key-per-wave kernels.
+template <int DMAX, int D, bool NODES, bool PAIR, bool B>
 __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
     if constexpr (PAIR && D == 3) {
         // Lane pairs write whole 128-B lines.  Lanes 2i and 2i+1 own adjacent
@@ -195,15 +204,17 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         // lane computes them.
         CW cw = load_cw(c.ek, lvl0 + DMAX - 3);
         Node L, R;
-        expand(c.tab, c.lo, n, cw, L, R);
+        expand<B>(c.tab, c.lo, n, cw, L, R);
         const bool odd = (threadIdx.x & 1u) != 0;
         const Node got = pair_swap(sel(odd, L, R));   // even gets L(Nb), odd gets R(Na)
         const int64_t sub = 16ll << DMAX;
-        const Node first = sel(odd, got, L), second = sel(odd, R, got);
+        Node cur = sel(odd, got, L);
+        const Node second = sel(odd, R, got);
 #pragma nounroll
-        for (int h = 0; h < 2; ++h)   // one code copy of leaves4 (instruction cache)
-            leaves4(c, lvl0 + DMAX - 2, sel(h == 0, first, second),
-                    c.outp + (h == 0 ? (odd ? 64 - sub : 0) : (odd ? 64 : sub)));
+        for (int h = 0; h < 2; ++h) {   // one code copy of leaves4 (instruction cache)
+            leaves4<B>(c, lvl0 + DMAX - 2, cur, c.outp + (h == 0 ? (odd ? 64 - sub : 0) : (odd ? 64 : sub)));
+            cur = second;
+        }
         c.outp += 128;
     } else if constexpr (D == 0) {
         if constexpr (NODES) {
@@ -216,7 +227,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
     } else if constexpr (D == 2 && !NODES) {
         // Bottom two levels at once: 4 leaves = 64 contiguous bytes stored back
         // to back (subtrees too shallow or lanes of different keys for PAIR).
-        leaves4(c, lvl0 + DMAX - 2, n, c.outp);
+        leaves4<B>(c, lvl0 + DMAX - 2, n, c.outp);
         c.outp += 64;
     } else if constexpr (D == 2 && NODES) {
         // Bottom two levels of a frontier at once: 4 seeds = 64 contiguous
@@ -224,11 +235,11 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         // node made the NODES pass write 2.2x its 17 B per node).
         CW cw = load_cw(c.ek, lvl0 + DMAX - 2);
         Node L, R;
-        expand(c.tab, c.lo, n, cw, L, R);
+        expand<B>(c.tab, c.lo, n, cw, L, R);
         CW cw1 = load_cw(c.ek, lvl0 + DMAX - 1);
         Node q[4];
-        expand(c.tab, c.lo, L, cw1, q[0], q[1]);
-        expand(c.tab, c.lo, R, cw1, q[2], q[3]);
+        expand<B>(c.tab, c.lo, L, cw1, q[0], q[1]);
+        expand<B>(c.tab, c.lo, R, cw1, q[2], q[3]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) c.nseed[i] = make_uint4(q[i].s.c0, q[i].s.c1, q[i].s.c2, q[i].s.c3);
         *reinterpret_cast<uint32_t*>(c.nt) = (q[0].t & 0xffu) | ((q[1].t & 0xffu) << 8) | ((q[2].t & 0xffu) << 16) |
@@ -238,13 +249,13 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
     } else if constexpr (D == 1) {
         CW cw = load_cw(c.ek, lvl0 + DMAX - 1);
         Node L, R;
-        expand(c.tab, c.lo, n, cw, L, R);
+        expand<B>(c.tab, c.lo, n, cw, L, R);
         if constexpr (NODES) {
             emit_node(c, L);
             emit_node(c, R);
         } else {
             Blk oL, oR;
-            mmo_pair(c.tab, c.lo, KeyFixed<false>{}, L.s, oL, KeyFixed<false>{}, R.s, oR);
+            mmo_pair<B>(c.tab, c.lo, KeyFixed<false>{}, L.s, oL, KeyFixed<false>{}, R.s, oR);
             store16(c.outp, leaf_fix(oL, L.t, c.fcw));
             store16(c.outp + 16, leaf_fix(oR, R.t, c.fcw));
             c.outp += 32;
@@ -252,16 +263,14 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
     } else {
         CW cw = load_cw(c.ek, lvl0 + DMAX - D);
         Node L, R;
-        expand(c.tab, c.lo, n, cw, L, R);
+        expand<B>(c.tab, c.lo, n, cw, L, R);
+        // The right child is the only node live across the left subtree.
+        Node ch = L;
+        const Node pend = R;
 #pragma nounroll
         for (int side = 0; side < 2; ++side) {
-            Node ch;
-            ch.s.c0 = side ? R.s.c0 : L.s.c0;
-            ch.s.c1 = side ? R.s.c1 : L.s.c1;
-            ch.s.c2 = side ? R.s.c2 : L.s.c2;
-            ch.s.c3 = side ? R.s.c3 : L.s.c3;
-            ch.t = side ? R.t : L.t;
-            dfs<DMAX, D - 1, NODES, PAIR>(c, lvl0, ch);
+            dfs<DMAX, D - 1, NODES, PAIR, B>(c, lvl0, ch);
+            ch = pend;
         }
     }
 }
@@ -367,7 +376,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     // leaf stores (dfs PAIR).  DPF_PAIR_STORES=0 builds the r02 half-line
     // stores for A/B runs.
     constexpr bool kPair = DPF_PAIR_STORES && UNIFORM && !NODES && D >= 3;
-    dfs<D, D, NODES, kPair>(c, ltop, n);
+    dfs<D, D, NODES, kPair, UNIFORM>(c, ltop, n);
 }
 
 // Batched Eval: one thread per query, independent walks that compute only
@@ -425,7 +434,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_mmo_tt(const uint4* __restrict__ 
     const uint32_t lo = (threadIdx.x & 31u) * 4u;
     const uint4 va = in[2 * u], vb = in[2 * u + 1];
     Blk a = {va.x, va.y, va.z, va.w}, b = {vb.x, vb.y, vb.z, vb.w};
-    for (uint32_t r = 0; r < reps; ++r) mmo_pair(tab, lo, KeyFixed<RIGHT>{}, a, a, KeyFixed<RIGHT>{}, b, b);
+    for (uint32_t r = 0; r < reps; ++r) mmo_pair<true>(tab, lo, KeyFixed<RIGHT>{}, a, a, KeyFixed<RIGHT>{}, b, b);
     out[2 * u] = make_uint4(a.c0, a.c1, a.c2, a.c3);
     out[2 * u + 1] = make_uint4(b.c0, b.c1, b.c2, b.c3);
 }
