@@ -149,11 +149,19 @@ __device__ __forceinline__ void round_mix(const K& k, const uint32_t (&t)[16], B
     s.c3 = col(3, k.template get16<4 * R + 3>());
 }
 
-template <int R, class K>
+template <int R, bool BATCH = false, class K>
 __device__ __forceinline__ void aes_rounds(const uint8_t* tab, uint32_t lo, const K& k, Blk& s) {
     if constexpr (R <= 9) {
-        aes_round<R>(tab, lo, k, s);
-        aes_rounds<R + 1>(tab, lo, k, s);
+        if constexpr (BATCH) {
+            uint32_t t[16];
+            round_loads(tab, lo, s, t);
+            __builtin_amdgcn_sched_barrier(0);
+            round_mix<R>(k, t, s);
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            aes_round<R>(tab, lo, k, s);
+        }
+        aes_rounds<R + 1, BATCH>(tab, lo, k, s);
     }
 }
 
@@ -182,10 +190,10 @@ __device__ __forceinline__ Blk bxor(Blk a, Blk b) { return {a.c0 ^ b.c0, a.c1 ^ 
 __device__ __forceinline__ Blk bkey4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return {a, b, c, d}; }
 
 // aes128MMO (aes_amd64.s:51-82): AES_k(x) ^ x.
-template <class K>
+template <bool BATCH = false, class K>
 __device__ __forceinline__ Blk mmo1(const uint8_t* tab, uint32_t lo, const K& k, Blk x) {
     Blk s = bxor(x, bkey4(k.template get<0>(), k.template get<1>(), k.template get<2>(), k.template get<3>()));
-    aes_rounds<1>(tab, lo, k, s);
+    aes_rounds<1, BATCH>(tab, lo, k, s);
     aes_last(tab, lo, k, s);
     return bxor(s, x);
 }

@@ -28,6 +28,9 @@
 #ifndef DPF_MMO_INTERLEAVE
 #define DPF_MMO_INTERLEAVE 1
 #endif
+#ifndef DPF_EVAL_BATCH
+#define DPF_EVAL_BATCH 1
+#endif
 
 namespace dpfk {
 
@@ -91,9 +94,10 @@ __device__ __forceinline__ void expand(const uint8_t* tab, uint32_t lo, const No
 
 // One step of a root-to-node walk that computes only the child selected by
 // `bit` (dpf.go:183-201, minus the unused sibling).
+template <bool B = false>
 __device__ __forceinline__ void walk_step(const uint8_t* tab, uint32_t lo, Node& n, const CW& cw, uint32_t bit) {
     uint32_t kb = bit ? 0xffffffffu : 0u;
-    Blk c = mmo1(tab, lo, KeySel{kb}, n.s);
+    Blk c = mmo1<B>(tab, lo, KeySel{kb}, n.s);
     uint32_t tc = c.c0 & 1u;
     c.c0 &= ~1u;
     uint32_t m = tmask(n.t);
@@ -412,9 +416,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     }
     for (uint32_t i = lvl; i < stop; ++i) {
         CW cw = load_cw(ek, i);
-        walk_step(tab, lo, n, cw, (uint32_t)(x >> (logN - 1 - i)) & 1u);
+        walk_step<DPF_EVAL_BATCH>(tab, lo, n, cw, (uint32_t)(x >> (logN - 1 - i)) & 1u);
     }
-    Blk o = mmo1(tab, lo, KeyFixed<false>{}, n.s);
+    Blk o = mmo1<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n.s);
     o = leaf_fix(o, n.t, load_blk(ek + 8 + 8 * stop));
     const uint32_t b = (uint32_t)(x & 127);
     const uint32_t w = (b >> 5) == 0 ? o.c0 : (b >> 5) == 1 ? o.c1 : (b >> 5) == 2 ? o.c2 : o.c3;

@@ -1,11 +1,24 @@
 #!/bin/bash
-# Batched Eval variants at configs[2] (HBM frontier default, LDS frontier, plain root walks).
+# A/B of tree-kernel build variants on the Eval workload (configs[2]),
+# interleaved over 3 rounds, plus a kernel trace per variant.
+#   tools/exp_eval.sh <out_tag> <variant>...   ("base" = product build)
 set -uo pipefail
-mkdir -p gpurun_out/exp2
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/exp2/gpu_tests.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/exp2/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-for m in hbm lds plain; do
-  DPF_EVAL_MODE=$m timeout -k 10 300 python bench.py --workload eval --steps 20 --warmup 5 --check \
-      > gpurun_out/exp2/eval_$m.log 2>&1 || exit 1
-  echo "$m $(grep -o '"value": [0-9.e+]*' gpurun_out/exp2/eval_$m.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/exp2/eval_$m.log)"
+REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$REPO"
+OUT="gpurun_out/$1"; shift
+mkdir -p "$OUT"
+B=(--workload eval --steps 30 --warmup 5 --spinup 0.5 --no-cpu-baseline --no-variants --no-api --aes ttable)
+lib() { if [ "$1" = base ]; then echo "$REPO/dpf-go_amd/lib/libdpf_hip.so"; else echo "$REPO/tools/bin/libdpf_hip_$1.so"; fi; }
+for r in 1 2 3; do
+  for v in "$@"; do
+    DPF_LIB=$(lib $v) timeout -k 10 200 python bench.py "${B[@]}" --check > "$OUT/${v}_$r.log" 2>&1 || { echo "FAIL $v"; tail -5 "$OUT/${v}_$r.log"; exit 1; }
+    grep '^{' "$OUT/${v}_$r.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v r$r', round(d['ms_per_step'],4), d['value'])"
+  done
+done
+export TMPDIR=/tmp
+for v in "$@"; do
+  ( cd /tmp && DPF_LIB=$(lib $v) timeout -k 10 150 rocprofv3 --kernel-trace --stats -d "$REPO/$OUT/t_$v" -o t --output-format csv -- \
+      python3 "$REPO/bench.py" --workload eval --steps 10 --warmup 2 --no-cpu-baseline --no-variants --no-api --aes ttable > "$REPO/$OUT/t_$v.log" 2>&1 ) || { echo "trace FAIL $v"; exit 1; }
+  f=$(find "$REPO/$OUT/t_$v" -name '*kernel_stats.csv' | head -1)
+  echo "$v"; grep -E 'k_eval|k_evalfull' "$f" | cut -d, -f1-6
 done
