@@ -1,0 +1,575 @@
+// pir_kernels.hip — XOR-fold of records selected by EvalFull bits on gfx950:
+// the 2-server PIR answer (last row: a build-only operator with
+// no reference counterpart) and its general-payload form.
+//
+//   ans_k = XOR over records i with bit_i(EvalFull(key_k)) = 1 of DB[i]
+//
+// Phase 1 (dpf_kernels.hip, subtree EvalFull) writes each key's selection
+// bits into HBM: bits[k][i/32] bit (i%32), which is exactly EvalFull's packed
+// LSB-first byte layout (dpf/dpf.go:248-261) read as little-endian u32.
+// Phase 2 (here) reads every record once from HBM per launch and folds it
+// into all of the launch's answers.  The fold is a GF(2) product and stays
+// bitwise (VALU XOR + LDS table lookups); it is not reshaped into an int8
+// MFMA GEMM (8x data expansion for the same HBM-bound stream).
+//
+// Work unit.  A "chunk" is 64 records (one 64-bit word pair of every key's
+// selection bits); a record is C 32-byte columns (C = rec_bytes / 32).  A
+// chunk is processed as C "sub-steps" of 2 KiB of contiguous DB bytes (64/C
+// records x all C columns), loaded by one wave as two coalesced 1 KiB loads:
+// lane l holds 16-byte pieces p = l and p = 64 + l.  Records of any other
+// multiple of 32 B run as C = 1 over one 32-byte column at a time (rec_u4 /
+// col below), one launch per column.
+//
+// Two kernels, chosen by batch size (launch_pir_fold):
+//   k_fold_direct  B <= 16 keys: each lane XORs its pieces into per-key
+//                  accumulators under the key's selection bit (selection
+//                  words come through scalar loads, uniform per wave).
+//                  ~10 VALU per key per 2 KiB: HBM-bound up to 16 keys.
+//   k_fold4r       B > 16: Four-Russians.  Per 4-record group and 32-byte
+//                  column a 16-entry table (entry e = XOR of the records
+//                  whose bit is set in e) is built in LDS once per wave and
+//                  looked up by up to 4 x 64 keys (lane = key): 2
+//                  ds_read_b128 per key per group instead of 32 masked XORs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pir_kernels.hpp"
+
+namespace dpfk {
+
+// v_bitop3_b32 truth tables: src0 = 0xF0, src1 = 0xCC, src2 = 0xAA.
+constexpr uint8_t kTT0 = 0xF0, kTT1 = 0xCC, kTT2 = 0xAA;
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, kTT0 ^ kTT1 ^ kTT2);
+}
+// a ^ (b & m)
+__device__ __forceinline__ uint32_t xam(uint32_t a, uint32_t b, uint32_t m) {
+    return __builtin_amdgcn_bitop3_b32(a, b, m, kTT0 ^ (kTT1 & kTT2));
+}
+__device__ __forceinline__ uint4 x4(uint4 a, uint4 b) { return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w); }
+__device__ __forceinline__ uint4 x4am(uint4 a, uint4 b, uint32_t m) {
+    return make_uint4(xam(a.x, b.x, m), xam(a.y, b.y, m), xam(a.z, b.z, m), xam(a.w, b.w, m));
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Piece p (0..127) of sub-step q of chunk cc, as a 16-byte index into the DB.
+// C > 1: contiguous records; C == 1: record stride rec_u4, column col (any
+// record width that is a multiple of 32 B).  Indices past the end are
+// clamped to the last record (its selection bit is masked off).
+template <int C>
+__device__ __forceinline__ uint64_t piece_index(uint64_t cc, uint32_t q, uint32_t p, uint64_t nrec, uint64_t rec_u4,
+                                                uint32_t col) {
+    if constexpr (C == 1) {
+        uint64_t r = cc * 64 + (p >> 1);
+        if (r >= nrec) r = nrec - 1;
+        return r * rec_u4 + 2 * col + (p & 1);
+    } else {
+        const uint64_t last = nrec * 2 * C - 1;
+        const uint64_t i = (cc * C + q) * 128 + p;
+        return i < last ? i : last;
+    }
+}
+
+// Bits of chunk cc's records below nrec, for word 0 (records 0..31) and 1;
+// none when the chunk is not the caller's (live = false).  Arithmetic, not
+// branches: a branch here splits the lookup block and the register
+// allocator then spills the table reads around it.
+__device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool live = true) {
+    uint64_t v = nrec > cc * 64 ? nrec - cc * 64 : 0;
+    v = live ? (v < 64 ? v : 64) : 0;
+    const uint32_t lo = v < 32 ? (uint32_t)v : 32u, hi = v > 32 ? (uint32_t)v - 32u : 0u;
+    return make_uint2((uint32_t)((1ull << lo) - 1), (uint32_t)((1ull << hi) - 1));
+}
+
+// ---------------------------------------------------------------------------
+// k_fold_direct<C, KB>: up to KB keys per launch, 4 waves per workgroup, each
+// wave takes every 4th chunk of the workgroup's contiguous range.  Lane l
+// always holds the same 16-byte position u = l mod 2C of its records, so its
+// accumulators are 4 words per key, XOR-reduced across lanes at the end.
+#ifndef DPF_FOLD_PIPE
+#define DPF_FOLD_PIPE 1   // table pairs in flight per wave in k_fold4r's lookups (2: no gain, fold_bench r03)
+#endif
+constexpr int kDWaves = 4;
+constexpr int kDirectMaxKeys = 16;
+
+template <int C, int KB>
+__global__ __launch_bounds__(64 * kDWaves) void k_fold_direct(const uint32_t* __restrict__ bits, uint64_t wpk,
+                                                             const uint4* __restrict__ db, uint64_t nrec,
+                                                             uint64_t rec_u4, uint32_t col, uint32_t nkeys,
+                                                             uint64_t chunks_per_block, uint32_t* __restrict__ parts) {
+    __shared__ uint32_t s_comb[kDWaves][KB][2 * C][4];
+    const uint32_t l = threadIdx.x & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nchunks = (nrec + 63) / 64;
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunks_per_block;
+    const uint64_t cend = c0 + chunks_per_block < nchunks ? c0 + chunks_per_block : nchunks;
+    uint32_t acc[KB][4];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
+    // Record (within the chunk) of sub-step q's pieces l (A) and 64 + l (B).
+    const uint32_t rA0 = l / (2 * C);
+    // Selection words travel like the pieces: lane l loads key (l mod KB)'s
+    // word pair of a chunk together with the chunk's first sub-step (vector
+    // loads, one chunk ahead), and v_readlane hands each key's pair to the
+    // wave as scalars.  (Per-key scalar loads were each waited on where used.)
+    const uint32_t skey = (l % KB) < nkeys ? (l % KB) : 0;
+    auto load = [&](uint64_t cc, uint32_t q, uint4& A, uint4& B, uint2& S) __attribute__((always_inline)) {
+        A = db[piece_index<C>(cc, q, l, nrec, rec_u4, col)];
+        B = db[piece_index<C>(cc, q, 64 + l, nrec, rec_u4, col)];
+        if (q == 0) {
+            const uint64_t cs = cc < nchunks ? cc : nchunks - 1;
+            S = *reinterpret_cast<const uint2*>(bits + skey * wpk + 2 * cs);
+        }
+    };
+    // Items (chunk, sub-step) in pairs of chunks: 2C items, so the two load
+    // buffers alternate by item parity and the next item's pieces are in
+    // flight while this one is folded.  Every step issues its loads and XORs
+    // unconditionally (indices clamped, selection bits masked): a branch
+    // around a prefetch makes the compiler drain every load (s_waitcnt
+    // vmcnt(0)) at the join.
+    uint4 A0, B0, A1, B1;
+    uint2 S0 = make_uint2(0, 0), S1 = make_uint2(0, 0);
+    load(c0 + w, 0, A0, B0, S0);
+    uint2 sel[KB];
+    auto step = [&](uint64_t cp, int i, const uint4& A, const uint4& B, const uint2& S, uint4& NA, uint4& NB,
+                    uint2& NS) __attribute__((always_inline)) {
+        const uint64_t cc = cp + (uint64_t)(i / C) * kDWaves;
+        const uint32_t q = (uint32_t)(i % C);
+        const uint64_t nc = i + 1 < 2 * C ? cp + (uint64_t)((i + 1) / C) * kDWaves : cp + 2 * kDWaves;
+        const uint32_t nq = i + 1 < 2 * C ? (uint32_t)((i + 1) % C) : 0;
+        if (q == 0) {
+            const uint2 vm = valid_mask(cc, nrec, cc < cend);
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                const bool live = (uint32_t)k < nkeys;
+                const uint32_t sx = __builtin_amdgcn_readlane(S.x, k), sy = __builtin_amdgcn_readlane(S.y, k);
+                sel[k] = make_uint2(live ? sx & vm.x : 0u, live ? sy & vm.y : 0u);
+            }
+        }
+        load(nc, nq, NA, NB, NS);
+        // Records of A and B: 64q/C + rA0 and that + 32/C.  For C = 1 they are
+        // in words 0 and 1; for C >= 2 both are in word 2q/C.
+        const uint32_t rA = (64 * q) / C + rA0, rB = rA + 32 / C;
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            const uint32_t wA = C == 1 ? sel[k].x : ((2 * q) / C ? sel[k].y : sel[k].x);
+            const uint32_t wB = C == 1 ? sel[k].y : wA;
+            const uint32_t mA = 0u - ((wA >> (rA & 31)) & 1u);
+            const uint32_t mB = 0u - ((wB >> (rB & 31)) & 1u);
+            acc[k][0] = xam(xam(acc[k][0], A.x, mA), B.x, mB);
+            acc[k][1] = xam(xam(acc[k][1], A.y, mA), B.y, mB);
+            acc[k][2] = xam(xam(acc[k][2], A.z, mA), B.z, mB);
+            acc[k][3] = xam(xam(acc[k][3], A.w, mA), B.w, mB);
+        }
+    };
+    for (uint64_t cp = c0 + w; cp < cend; cp += 2 * kDWaves) {
+#pragma unroll
+        for (int i = 0; i < 2 * C; i += 2) {
+            step(cp, i, A0, B0, S0, A1, B1, S1);
+            step(cp, i + 1, A1, B1, S1, A0, B0, S0);
+        }
+    }
+    // Lanes with the same position u = l mod 2C hold partial XORs of the same words.
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            uint32_t v = acc[k][d];
+#pragma unroll
+            for (int off = 2 * C; off < 64; off *= 2) v ^= (uint32_t)__shfl_xor((int)v, off, 64);
+            acc[k][d] = v;
+        }
+    }
+    if (l < 2 * C) {
+#pragma unroll
+        for (int k = 0; k < KB; ++k)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) s_comb[w][k][l][d] = acc[k][d];
+    }
+    __syncthreads();
+    // parts[block][key][8C words]; word 4u + d of a key's answer is position u, dword d.
+    constexpr uint32_t words = (uint32_t)KB * 8 * C;
+    for (uint32_t t = threadIdx.x; t < words; t += blockDim.x) {
+        const uint32_t k = t / (8 * C), u = (t / 4) % (2 * C), d = t % 4;
+        uint32_t v = 0;
+#pragma unroll
+        for (int ww = 0; ww < kDWaves; ++ww) v ^= s_comb[ww][k][u][d];
+        parts[(uint64_t)blockIdx.x * words + t] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fold4r<C, KW, WV>: Four-Russians over 64*KW keys (lane l = keys l, 64+l,
+// ...), WV waves per workgroup.  Per sub-step the wave owns 16 tables (4-record
+// group gs x column cl, t = gs*C + cl), each two 256-byte rows (half h of the
+// 32-byte column) of 16 slots:
+//   stage : the loaded pieces go straight to their single-record slots
+//           (entries 1, 2, 4, 8); entry 0 is a zero written once;
+//   build : lanes 4t .. 4t+3 (h = l&1, a = (l>>1)&1) read the row's 4 records
+//           and write the other 11 entries, 6 stores per lane;
+//   lookup: each key-lane takes the group's 4 selection bits -- a nibble of
+//           EvalFull's LSB-first layout -- as the entry index and XORs the
+//           32-byte entry (2 ds_read_b128) into column cl's accumulator.
+// Slot of entry e in row (t, h): f(e) ^ sw(t, h), f linear with f(8) = 11,
+// sw = 2[t&1] ^ 1[t&2] ^ 4h (searched exhaustively): every staging store,
+// build read and build store is conflict-free in its lane groups (8-lane
+// groups over 32 banks for ds_write_b128, the 16-lane groups of ds_read_b128
+// over 64 banks), lookups read one row and f is a bijection.
+// The build is amortised over all 64*KW keys, so a B = 256 batch reads the DB
+// once with 1/4 of the per-key table work of B = 64.
+
+__host__ __device__ constexpr uint32_t f_slot(uint32_t e) { return e ^ (((e >> 3) & 1u) * 3u); }
+__host__ __device__ constexpr uint32_t sw_row(uint32_t t, uint32_t h) {
+    return ((t & 1u) ? 2u : 0u) ^ ((t & 2u) ? 1u : 0u) ^ (h ? 4u : 0u);
+}
+
+template <int WV>
+struct Fold4rCfg {
+    static constexpr int batch = 2 * WV;          // chunks per selection batch: 16*WV bytes of a key's bits
+    static constexpr int sel_row = 4 * WV + 2;    // words per staged row (+2 pad: conflict-free ds_read_b64)
+};
+
+template <int C, int KW, int WV>
+__global__ __launch_bounds__(64 * WV, WV == 8 ? 4 : 3) void k_fold4r(const uint32_t* __restrict__ bits, uint64_t wpk,
+                                                                    const uint4* __restrict__ db, uint64_t nrec,
+                                                                    uint64_t rec_u4, uint32_t col, uint32_t nkeys,
+                                                                    uint64_t chunks_per_block,
+                                                                    uint32_t* __restrict__ parts) {
+    using Cfg = Fold4rCfg<WV>;
+    __shared__ uint4 s_tab[WV][32 * 16];                                   // 8 KiB per wave
+    __shared__ __attribute__((aligned(16))) uint32_t s_sel[KW * 64 * Cfg::sel_row];
+    const uint32_t l = threadIdx.x & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nchunks = (nrec + 63) / 64;
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunks_per_block;
+    const uint64_t cend = c0 + chunks_per_block < nchunks ? c0 + chunks_per_block : nchunks;
+    uint4* tab = s_tab[w];
+
+    // Entry 0 of every row: a zero slot, written once.
+    if (l < 32) tab[l * 16 + sw_row(l >> 1, l & 1)] = make_uint4(0, 0, 0, 0);
+    // Staging slots of this lane's pieces p = l (A) and 64 + l (B, table + 8).
+    const uint32_t pr = l / (2 * C), pcl = (l / 2) % C, ph = l & 1;
+    const uint32_t pt = (pr >> 2) * C + pcl, pi = pr & 3;
+    const uint32_t stA = (2 * pt + ph) * 16 + (f_slot(1u << pi) ^ sw_row(pt, ph));
+    const uint32_t stB = stA + 16 * 16;
+    // Build role: row (bt, bh), lane pair a.
+    const uint32_t bt = l >> 2, bh = l & 1, ba = (l >> 1) & 1;
+    uint4* brow = tab + (2 * bt + bh) * 16;
+    const uint32_t bsw = sw_row(bt, bh);
+    const uint32_t m0 = ba ? 0u : ~0u;
+
+    // Selection staging: thread t copies 16 B of key (kg*64 + t/WV)'s line.
+    const uint32_t sk = threadIdx.x / WV, sp = threadIdx.x % WV;
+    auto load_sel = [&](int kg, uint64_t cb) __attribute__((always_inline)) {
+        const uint32_t key = (uint32_t)kg * 64 + sk;
+        const uint32_t* srow = bits + (uint64_t)(key < nkeys ? key : 0) * wpk;
+        const uint64_t wo = cb * 2 + 4 * sp;                         // clamped, then zeroed: no branch
+        const uint4 v = *reinterpret_cast<const uint4*>(srow + (wo + 4 <= wpk ? wo : wpk - 4));
+        return wo + 4 <= wpk ? v : make_uint4(0, 0, 0, 0);
+    };
+    uint32_t keymask[KW];
+#pragma unroll
+    for (int kg = 0; kg < KW; ++kg) keymask[kg] = (uint32_t)kg * 64 + l < nkeys ? ~0u : 0u;
+
+    uint32_t acc[KW][C][8];
+#pragma unroll
+    for (int kg = 0; kg < KW; ++kg)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[kg][c][i] = 0;
+
+    auto fold = [&](uint64_t cc, uint32_t q, uint64_t cb, const uint4& A, const uint4& B) __attribute__((always_inline)) {
+        // stage
+        tab[stA] = A;
+        tab[stB] = B;
+        wave_sync();
+        // build: R_i = record i of this row's group
+        const uint4 R0 = brow[f_slot(1) ^ bsw], R1 = brow[f_slot(2) ^ bsw];
+        const uint4 R2 = brow[f_slot(4) ^ bsw], R3 = brow[f_slot(8) ^ bsw];
+        const uint4 R12 = x4(R1, R2), R13 = x4(R1, R3), R23 = x4(R2, R3), R123 = x4(R12, R3);
+        // a = 0 writes 7, 11, 13, 15, 3, 5; a = 1 writes 6, 10, 12, 14, 9.
+        brow[f_slot(7 ^ ba) ^ bsw] = x4am(R12, R0, m0);
+        brow[f_slot(11 ^ ba) ^ bsw] = x4am(R13, R0, m0);
+        brow[f_slot(13 ^ ba) ^ bsw] = x4am(R23, R0, m0);
+        brow[f_slot(15 ^ ba) ^ bsw] = x4am(R123, R0, m0);
+        const uint4 S = ba ? R3 : R1;
+        brow[f_slot(ba ? 9 : 3) ^ bsw] = x4(R0, S);
+        if (!ba) brow[f_slot(5) ^ bsw] = x4(R0, R2);
+        wave_sync();
+        // lookups
+        const uint32_t j = (uint32_t)(cc - cb);
+        const uint2 vm = valid_mask(cc, nrec);
+#pragma unroll
+        for (int kg = 0; kg < KW; ++kg) {
+            // One lane group at a time: interleaving their reads only spills.
+            if (kg) __builtin_amdgcn_sched_barrier(0);
+            uint2 sel = *reinterpret_cast<const uint2*>(&s_sel[(kg * 64 + l) * Cfg::sel_row + 2 * j]);
+            sel.x &= vm.x & keymask[kg];
+            sel.y &= vm.y & keymask[kg];
+            // Nibbles n of this sub-step: n = q*16/C + gs, gs < 16/C (word n >> 3).
+            // Pre-swizzle: f applied to every nibble.
+            auto fz = [](uint32_t z) __attribute__((always_inline)) {
+                const uint32_t m = (z >> 3) & 0x11111111u;
+                return z ^ m ^ (m << 1);
+            };
+            const uint32_t z0 = fz(sel.x), z1 = fz(sel.y);
+            // Tables t and t + C share column cl: one 3-input XOR per word for
+            // both (the bitop3 builtin also keeps the compiler from
+            // re-associating the chain).  The 8 pairs are software-pipelined:
+            // pair p + kPipe's 4 reads are issued before pair p's XORs, with
+            // scheduling fences so the compiler keeps that order (left alone,
+            // it reads one pair, waits, XORs: 4 reads in flight per wave).
+            auto slot = [&](uint32_t t) __attribute__((always_inline)) {
+                const uint32_t n = q * (16 / C) + t / C;
+                const uint32_t z = (n >> 3) ? z1 : z0;
+                return (z >> (4 * (n & 7))) & 15u;
+            };
+            // Two pairs in flight where the registers allow (measured: no spills).
+            constexpr int kPairs = 8;
+            constexpr int kPipe = (KW * C >= 8 && C < 8) || (WV == 8 && C >= 4) ? 1 : DPF_FOLD_PIPE;
+            uint4 rd[kPairs][4];
+            auto pair_t0 = [](int pi) { return (pi / C) * 2 * C + pi % C; };   // pair pi = tables (t0, t0 + C)
+            auto issue = [&](int pi) __attribute__((always_inline)) {
+                const uint32_t t0 = pair_t0(pi), t1 = t0 + C;
+                const uint32_t e0 = slot(t0), e1 = slot(t1);
+                rd[pi][0] = tab[(2 * t0) * 16 + (e0 ^ sw_row(t0, 0))];
+                rd[pi][1] = tab[(2 * t0 + 1) * 16 + (e0 ^ sw_row(t0, 1))];
+                rd[pi][2] = tab[(2 * t1) * 16 + (e1 ^ sw_row(t1, 0))];
+                rd[pi][3] = tab[(2 * t1 + 1) * 16 + (e1 ^ sw_row(t1, 1))];
+            };
+#pragma unroll
+            for (int pi = 0; pi < kPipe; ++pi) issue(pi);
+#pragma unroll
+            for (int pi = 0; pi < kPairs; ++pi) {
+                if (pi + kPipe < kPairs) issue(pi + kPipe);
+                __builtin_amdgcn_sched_barrier(0);
+                const uint4 lo0 = rd[pi][0], hi0 = rd[pi][1], lo1 = rd[pi][2], hi1 = rd[pi][3];
+                uint32_t* a = acc[kg][pair_t0(pi) % C];
+                a[0] = x3(a[0], lo0.x, lo1.x); a[1] = x3(a[1], lo0.y, lo1.y);
+                a[2] = x3(a[2], lo0.z, lo1.z); a[3] = x3(a[3], lo0.w, lo1.w);
+                a[4] = x3(a[4], hi0.x, hi1.x); a[5] = x3(a[5], hi0.y, hi1.y);
+                a[6] = x3(a[6], hi0.z, hi1.z); a[7] = x3(a[7], hi0.w, hi1.w);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        wave_sync();
+    };
+
+    // Batches of Cfg::batch chunks (one 16*WV-byte piece of every key's bits);
+    // each wave takes chunks cb + w and cb + WV + w of a batch, C sub-steps
+    // each.  Loads ping-pong between two buffers (2C items per batch, even),
+    // so the next sub-step's records are in flight during a fold.
+    auto load = [&](uint64_t cc, uint32_t q, uint4& A, uint4& B) __attribute__((always_inline)) {
+        A = db[piece_index<C>(cc, q, l, nrec, rec_u4, col)];
+        B = db[piece_index<C>(cc, q, 64 + l, nrec, rec_u4, col)];
+    };
+    uint4 A0, B0, A1, B1;
+    load(c0 + w, 0, A0, B0);
+    uint4 snext[KW];
+#pragma unroll
+    for (int kg = 0; kg < KW; ++kg) snext[kg] = load_sel(kg, c0);
+    auto step = [&](uint64_t cb, int i, const uint4& A, const uint4& B, uint4& NA, uint4& NB) __attribute__((always_inline)) {
+        const uint64_t cc = cb + w + (uint64_t)(i / C) * WV;
+        const uint32_t q = (uint32_t)(i % C);
+        const uint64_t nc = i + 1 < 2 * C ? cb + w + (uint64_t)((i + 1) / C) * WV : cb + Cfg::batch + w;
+        const uint32_t nq = i + 1 < 2 * C ? (uint32_t)((i + 1) % C) : 0;
+        load(nc, nq, NA, NB);            // unconditional (clamped): see k_fold_direct
+        if (cc < cend) fold(cc, q, cb, A, B);
+    };
+    for (uint64_t cb = c0; cb < cend; cb += Cfg::batch) {
+        __syncthreads();                                   // previous batch's selection reads are done
+#pragma unroll
+        for (int kg = 0; kg < KW; ++kg) {
+            uint32_t* row = &s_sel[(kg * 64 + sk) * Cfg::sel_row + 4 * sp];
+            *reinterpret_cast<uint2*>(row) = make_uint2(snext[kg].x, snext[kg].y);
+            *reinterpret_cast<uint2*>(row + 2) = make_uint2(snext[kg].z, snext[kg].w);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kg = 0; kg < KW; ++kg) snext[kg] = load_sel(kg, cb + Cfg::batch);
+#pragma unroll
+        for (int i = 0; i < 2 * C; i += 2) {
+            step(cb, i, A0, B0, A1, B1);
+            step(cb, i + 1, A1, B1, A0, B0);
+        }
+    }
+    // Combine the workgroup's waves in LDS (reusing the tables), one
+    // 8-word slice (key group, column) at a time: parts[block][key][8C words].
+    constexpr uint32_t pkeys = 64 * KW, pwords = 8 * C;
+    uint32_t* comb = reinterpret_cast<uint32_t*>(&s_tab[0][0]);     // [wave][lane][8]
+#pragma unroll
+    for (int kg = 0; kg < KW; ++kg)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) comb[(w * 64 + l) * 8 + i] = acc[kg][c][i];
+            __syncthreads();
+            for (uint32_t t = threadIdx.x; t < 64 * 8; t += blockDim.x) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int ww = 0; ww < WV; ++ww) v ^= comb[ww * 64 * 8 + t];
+                const uint32_t key = kg * 64 + t / 8;
+                parts[((uint64_t)blockIdx.x * pkeys + key) * pwords + c * 8 + (t % 8)] = v;
+            }
+        }
+}
+
+// ans[k * ans_words + off + i] ^= XOR over workgroups p of parts[p][k][i]
+// (k < nkeys, i < pwords; pkeys keys per part).  Block (x, y): 256 words x
+// parts y, y + gridDim.y, ...; one atomicXor each.
+__global__ __launch_bounds__(256) void k_xor_parts(const uint32_t* __restrict__ parts, uint64_t nparts, uint32_t nkeys,
+                                                   uint32_t pkeys, uint32_t pwords, uint32_t* __restrict__ ans,
+                                                   uint64_t ans_words, uint32_t off) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nkeys * pwords) return;
+    const uint32_t k = t / pwords, i = t % pwords;
+    uint32_t v = 0;
+    for (uint64_t p = blockIdx.y; p < nparts; p += gridDim.y) v ^= parts[(p * pkeys + k) * pwords + i];
+    if (v) atomicXor(ans + (uint64_t)k * ans_words + off + i, v);
+}
+
+static int cu_count_fold() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return cus;
+}
+
+constexpr uint64_t kFoldMaxBlocks = 1024;          // workgroups per launch (partials area)
+constexpr uint64_t kFoldPartBytes = 64 * 4 * 32 * 2;   // largest part: 64*KW keys x 32C bytes, KW*C <= 8
+
+uint64_t pir_fold_parts_bytes() { return kFoldMaxBlocks * kFoldPartBytes; }
+
+namespace {
+
+// Split nchunks into `blocks` contiguous ranges of whole `gran`-chunk batches.
+void split_chunks(uint64_t nchunks, uint64_t want_blocks, uint64_t gran, uint64_t& blocks, uint64_t& cpb) {
+    if (want_blocks > kFoldMaxBlocks) want_blocks = kFoldMaxBlocks;
+    cpb = (nchunks + want_blocks - 1) / want_blocks;
+    cpb = (cpb + gran - 1) / gran * gran;
+    blocks = (nchunks + cpb - 1) / cpb;
+}
+
+struct FoldArgs {
+    const uint32_t* bits;
+    uint64_t wpk;
+    const uint4* db;
+    uint64_t nrec, rec_u4;
+    uint32_t col, nkeys;
+    uint32_t* parts;
+};
+
+template <int C, int KB>
+hipError_t launch_direct_kb(const FoldArgs& a, uint64_t nchunks, uint64_t& blocks, hipStream_t st) {
+    uint64_t cpb;
+    split_chunks(nchunks, (uint64_t)cu_count_fold() * 4, 2 * kDWaves, blocks, cpb);
+    hipLaunchKernelGGL((k_fold_direct<C, KB>), dim3((uint32_t)blocks), dim3(64 * kDWaves), 0, st, a.bits, a.wpk, a.db,
+                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts);
+    return hipGetLastError();
+}
+
+// The direct kernel's work is linear in its key slots: 1, 4 or 16 by batch.
+template <int C>
+hipError_t launch_direct(const FoldArgs& a, uint64_t nchunks, uint64_t& blocks, uint32_t& pkeys, hipStream_t st) {
+    if (a.nkeys <= 1) return pkeys = 1, launch_direct_kb<C, 1>(a, nchunks, blocks, st);
+    if (a.nkeys <= 4) return pkeys = 4, launch_direct_kb<C, 4>(a, nchunks, blocks, st);
+    return pkeys = kDirectMaxKeys, launch_direct_kb<C, kDirectMaxKeys>(a, nchunks, blocks, st);
+}
+
+template <int C, int KW>
+hipError_t launch_4r(const FoldArgs& a, uint64_t nchunks, uint64_t& blocks, hipStream_t st) {
+    // KW = 1, C < 8: 8 waves, 72 KiB of LDS -> 2 workgroups (16 waves, 128
+    // VGPRs) per CU.  Otherwise 4 waves, 41-50 KiB -> 3 per CU (168 VGPRs:
+    // 64 accumulators per lane).
+    constexpr int WV = KW == 1 && C < 8 ? 8 : 4;
+    const uint64_t per_cu = WV == 8 ? 2 : 3;
+    uint64_t cpb;
+    split_chunks(nchunks, (uint64_t)cu_count_fold() * per_cu, 2 * WV, blocks, cpb);
+    hipLaunchKernelGGL((k_fold4r<C, KW, WV>), dim3((uint32_t)blocks), dim3(64 * WV), 0, st, a.bits, a.wpk, a.db,
+                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts);
+    return hipGetLastError();
+}
+
+// One pass over the DB for `a.nkeys` keys (<= 64*KW or <= 16 direct) with C
+// columns per record: fold kernel, then k_xor_parts into ans.
+template <int C>
+hipError_t fold_pass(const FoldArgs& a, bool direct, int kw, uint32_t* ans, uint64_t ans_words, uint32_t off,
+                     hipStream_t st) {
+    const uint64_t nchunks = (a.nrec + 63) / 64;
+    uint64_t blocks = 0;
+    uint32_t pkeys;
+    hipError_t e;
+    if (direct) {
+        e = launch_direct<C>(a, nchunks, blocks, pkeys, st);
+    } else if (kw >= 4) {
+        if constexpr (C <= 2) e = launch_4r<C, 4>(a, nchunks, blocks, st);
+        else return hipErrorInvalidValue;
+        pkeys = 256;
+    } else if (kw == 2) {
+        if constexpr (C <= 4) e = launch_4r<C, 2>(a, nchunks, blocks, st);
+        else return hipErrorInvalidValue;
+        pkeys = 128;
+    } else {
+        e = launch_4r<C, 1>(a, nchunks, blocks, st);
+        pkeys = 64;
+    }
+    if (e != hipSuccess) return e;
+    const uint32_t pwords = 8 * C;
+    const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
+    hipLaunchKernelGGL(k_xor_parts, dim3((a.nkeys * pwords + 255) / 256, ys), dim3(256), 0, st, a.parts, blocks,
+                       a.nkeys, pkeys, pwords, ans, ans_words, off);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+FoldPlan plan_fold(uint64_t rec_bytes, uint32_t nkeys) {
+    FoldPlan p{};
+    const uint64_t c = rec_bytes / 32;
+    p.cols = (c == 1 || c == 2 || c == 4 || c == 8) ? (uint32_t)c : 1;
+    p.col_passes = p.cols == c ? 1 : (uint32_t)c;
+    // Measured (tools/fold_bench, 2^24 x 32 B): direct is HBM-bound to 4 keys
+    // (98 -> 101 us) but slower than Four-Russians from 8 (150 vs ~140 us);
+    // wider records favour it longer (64 B, 16 keys: 69 us).
+    p.direct = nkeys <= 4 || (p.cols >= 2 && nkeys <= (uint32_t)kDirectMaxKeys);
+    const uint32_t kw_cap = p.cols >= 8 ? 1 : p.cols == 4 ? 2 : 4;
+    uint32_t kw = 1;
+    if (!p.direct)
+        while (kw < kw_cap && 64u * kw < nkeys) kw *= 2;
+    p.keys_per_pass = p.direct ? (uint32_t)kDirectMaxKeys : 64 * kw;
+    p.kw = p.direct ? 0 : kw;
+    return p;
+}
+
+hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const uint8_t* db, uint64_t nrec,
+                           uint64_t rec_bytes, uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
+    if (nrec == 0 || nkeys == 0) return hipSuccess;
+    if (rec_bytes == 0 || rec_bytes % 32 != 0) return hipErrorInvalidValue;
+    const FoldPlan p = plan_fold(rec_bytes, nkeys);
+    const uint64_t rec_u4 = rec_bytes / 16, ans_words = rec_bytes / 4;
+    for (uint32_t col = 0; col < p.col_passes; ++col)
+        for (uint32_t k0 = 0; k0 < nkeys; k0 += p.keys_per_pass) {
+            const uint32_t nk = nkeys - k0 < p.keys_per_pass ? nkeys - k0 : p.keys_per_pass;
+            FoldArgs a{bits + (uint64_t)k0 * words_per_key, words_per_key, reinterpret_cast<const uint4*>(db),
+                       nrec,  rec_u4, col, nk, parts};
+            uint32_t* an = ans + (uint64_t)k0 * ans_words;
+            hipError_t e;
+            switch (p.cols) {
+                case 2: e = fold_pass<2>(a, p.direct, (int)p.kw, an, ans_words, 0, st); break;
+                case 4: e = fold_pass<4>(a, p.direct, (int)p.kw, an, ans_words, 0, st); break;
+                case 8: e = fold_pass<8>(a, p.direct, (int)p.kw, an, ans_words, 0, st); break;
+                default: e = fold_pass<1>(a, p.direct, (int)p.kw, an, ans_words, 8 * col, st); break;
+            }
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+}  // namespace dpfk
