@@ -931,8 +931,11 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     if (nrec > slice) return fail(DPF_ERR_PARAM, "dpf: more DB records than the subtree's domain");
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(d_ans, 0, nkeys * 32, st));
-    if (nkeys == 0 || nrec == 0) return DPF_OK;
+    if (nkeys == 0) return DPF_OK;
+    if (nrec == 0) {
+        HIP_TRY(hipMemsetAsync(d_ans, 0, nkeys * 32, st));
+        return DPF_OK;
+    }
     // [tree workspace | selection bits = EvalFull bytes of the subtree | fold partials]
     const TreeWs w = tree_ws(d_work, nkeys, stop);
     uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
@@ -960,7 +963,6 @@ int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)stream;
     if (nkeys == 0) return DPF_OK;
-    HIP_TRY(hipMemsetAsync(d_ans, 0, nkeys * rec_bytes, st));
     HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)d_bits, bits_stride / 4, d_payload, nrec, rec_bytes, (uint32_t)nkeys,
                                   (uint32_t*)d_ans, (uint32_t*)d_work, st));
     return DPF_OK;

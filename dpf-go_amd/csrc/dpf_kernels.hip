@@ -31,6 +31,9 @@
 #ifndef DPF_EVAL_BATCH
 #define DPF_EVAL_BATCH 1
 #endif
+#ifndef DPF_WALK_BATCH
+#define DPF_WALK_BATCH 1   // tree kernels' root-to-subtree walks: batched single-block rounds
+#endif
 
 namespace dpfk {
 
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
                 Node m = n;
                 for (uint32_t i = 0; i < l1; ++i) {
                     CW cw = load_cw(ek, i);
-                    walk_step(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
+                    walk_step<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
                 }
                 uint32_t* f = s_front + 5 * threadIdx.x;
                 f[0] = m.s.c0; f[1] = m.s.c1; f[2] = m.s.c2; f[3] = m.s.c3; f[4] = m.t;
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     }
     for (uint32_t i = lvl; i < ltop; ++i) {
         CW cw = load_cw(ek, i);
-        walk_step(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
+        walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
     // Lane pairs share a key when a wave owns one key (UNIFORM): whole-line
     // leaf stores (dfs PAIR).  DPF_PAIR_STORES=0 builds the r02 half-line

@@ -50,6 +50,13 @@ __device__ __forceinline__ uint4 x4(uint4 a, uint4 b) { return make_uint4(a.x ^ 
 __device__ __forceinline__ uint4 x4am(uint4 a, uint4 b, uint32_t m) {
     return make_uint4(xam(a.x, b.x, m), xam(a.y, b.y, m), xam(a.z, b.z, m), xam(a.w, b.w, m));
 }
+// The first fold launch of a call clears the answers (instead of a separate
+// memset launch); k_xor_parts runs after it in stream order.
+__device__ __forceinline__ void zero_answers(uint32_t* zero, uint64_t words) {
+    if (zero == nullptr) return;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x)
+        zero[t] = 0;
+}
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -100,7 +107,9 @@ template <int C, int KB>
 __global__ __launch_bounds__(64 * kDWaves) void k_fold_direct(const uint32_t* __restrict__ bits, uint64_t wpk,
                                                              const uint4* __restrict__ db, uint64_t nrec,
                                                              uint64_t rec_u4, uint32_t col, uint32_t nkeys,
-                                                             uint64_t chunks_per_block, uint32_t* __restrict__ parts) {
+                                                             uint64_t chunks_per_block, uint32_t* __restrict__ parts,
+                                                             uint32_t* __restrict__ zero, uint64_t zero_words) {
+    zero_answers(zero, zero_words);
     __shared__ uint32_t s_comb[kDWaves][KB][2 * C][4];
     const uint32_t l = threadIdx.x & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -238,7 +247,9 @@ __global__ __launch_bounds__(64 * WV, WV == 8 ? 4 : 3) void k_fold4r(const uint3
                                                                     const uint4* __restrict__ db, uint64_t nrec,
                                                                     uint64_t rec_u4, uint32_t col, uint32_t nkeys,
                                                                     uint64_t chunks_per_block,
-                                                                    uint32_t* __restrict__ parts) {
+                                                                    uint32_t* __restrict__ parts,
+                                                                    uint32_t* __restrict__ zero, uint64_t zero_words) {
+    zero_answers(zero, zero_words);
     using Cfg = Fold4rCfg<WV>;
     __shared__ uint4 s_tab[WV][32 * 16];                                   // 8 KiB per wave
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[KW * 64 * Cfg::sel_row];
@@ -464,6 +475,8 @@ struct FoldArgs {
     uint64_t nrec, rec_u4;
     uint32_t col, nkeys;
     uint32_t* parts;
+    uint32_t* zero;          // first pass: the answers, cleared before k_xor_parts XORs into them
+    uint64_t zero_words;
 };
 
 template <int C, int KB>
@@ -471,7 +484,7 @@ hipError_t launch_direct_kb(const FoldArgs& a, uint64_t nchunks, uint64_t& block
     uint64_t cpb;
     split_chunks(nchunks, (uint64_t)cu_count_fold() * 4, 2 * kDWaves, blocks, cpb);
     hipLaunchKernelGGL((k_fold_direct<C, KB>), dim3((uint32_t)blocks), dim3(64 * kDWaves), 0, st, a.bits, a.wpk, a.db,
-                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts);
+                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts, a.zero, a.zero_words);
     return hipGetLastError();
 }
 
@@ -493,7 +506,7 @@ hipError_t launch_4r(const FoldArgs& a, uint64_t nchunks, uint64_t& blocks, hipS
     uint64_t cpb;
     split_chunks(nchunks, (uint64_t)cu_count_fold() * per_cu, 2 * WV, blocks, cpb);
     hipLaunchKernelGGL((k_fold4r<C, KW, WV>), dim3((uint32_t)blocks), dim3(64 * WV), 0, st, a.bits, a.wpk, a.db,
-                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts);
+                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts, a.zero, a.zero_words);
     return hipGetLastError();
 }
 
@@ -550,15 +563,20 @@ FoldPlan plan_fold(uint64_t rec_bytes, uint32_t nkeys) {
 
 hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const uint8_t* db, uint64_t nrec,
                            uint64_t rec_bytes, uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
-    if (nrec == 0 || nkeys == 0) return hipSuccess;
+    if (nkeys == 0) return hipSuccess;
     if (rec_bytes == 0 || rec_bytes % 32 != 0) return hipErrorInvalidValue;
+    if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * rec_bytes, st);
     const FoldPlan p = plan_fold(rec_bytes, nkeys);
     const uint64_t rec_u4 = rec_bytes / 16, ans_words = rec_bytes / 4;
     for (uint32_t col = 0; col < p.col_passes; ++col)
         for (uint32_t k0 = 0; k0 < nkeys; k0 += p.keys_per_pass) {
             const uint32_t nk = nkeys - k0 < p.keys_per_pass ? nkeys - k0 : p.keys_per_pass;
             FoldArgs a{bits + (uint64_t)k0 * words_per_key, words_per_key, reinterpret_cast<const uint4*>(db),
-                       nrec,  rec_u4, col, nk, parts};
+                       nrec,  rec_u4, col, nk, parts, nullptr, 0};
+            if (col == 0 && k0 == 0) {
+                a.zero = ans;
+                a.zero_words = (uint64_t)nkeys * ans_words;
+            }
             uint32_t* an = ans + (uint64_t)k0 * ans_words;
             hipError_t e;
             switch (p.cols) {

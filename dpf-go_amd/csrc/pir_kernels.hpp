@@ -18,9 +18,10 @@ struct FoldPlan {
 };
 FoldPlan plan_fold(uint64_t rec_bytes, uint32_t nkeys);
 
-// ans[k][0 .. rec_bytes) ^= XOR of the records db[i] (rec_bytes each, a
+// ans[k][0 .. rec_bytes) = XOR of the records db[i] (rec_bytes each, a
 // multiple of 32; i < nrec) whose bit i is set in bits[k * words_per_key
-// ...] (EvalFull's LSB-first layout).  `parts` is scratch of
+// ...] (EvalFull's LSB-first layout); zero when nrec == 0.  The first fold
+// launch clears ans itself (no separate memset).  `parts` is scratch of
 // pir_fold_parts_bytes() (per-workgroup partial answers).  bits, db 16-byte
 // aligned; words_per_key a multiple of 4 covering nrec bits.
 uint64_t pir_fold_parts_bytes();

@@ -49,11 +49,12 @@ def _fold(full_dev, stride, nk, payload, nrec, rec_bytes):
 # Every branch of the fold plan (pir_kernels.hip plan_fold): the direct kernel
 # (<= 16 keys) at 1/2/4/8 columns, Four-Russians with 1/2/4 lane groups per
 # table, several DB passes (> 256 keys, or C = 8 beyond 64 keys), widths that
-# run column by column (96, 160 B), ragged record counts and nrec = 1.
+# run column by column (96, 160 B), ragged record counts, nrec = 1 and nrec = 0
+# (answers cleared by the first fold launch, or by a memset when there is none).
 @pytest.mark.parametrize("logN,nk,rec_bytes,nrec", [
     (7, 3, 32, 128), (10, 5, 64, 1000), (12, 70, 96, 4096), (13, 9, 256, 5000), (14, 64, 32, 16384),
     (11, 16, 128, 2000), (11, 17, 128, 2000), (12, 130, 64, 4000), (12, 300, 32, 4096), (12, 100, 128, 3000),
-    (11, 70, 256, 2048), (9, 20, 32, 1), (13, 40, 160, 8000), (10, 1, 32, 777),
+    (11, 70, 256, 2048), (9, 20, 32, 1), (13, 40, 160, 8000), (10, 1, 32, 777), (10, 4, 64, 0),
 ])
 def test_xor_fold_matches_oracle(logN, nk, rec_bytes, nrec):
     import torch
