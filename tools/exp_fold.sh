@@ -10,7 +10,6 @@ for b in 1 4 8 16 17 32 64 128 256; do
   timeout -k 10 120 tools/fold_bench $b 32 24 >> $out/sweep.jsonl || exit 1
 done
 timeout -k 10 120 tools/bin/fold_bench_r02 64 32 24 >> $out/sweep.jsonl || exit 1
-timeout -k 10 120 tools/bin/fold_bench_p1 64 32 24 >> $out/sweep.jsonl || exit 1
 timeout -k 10 120 tools/bin/fold_bench_r02 256 32 24 >> $out/sweep.jsonl || exit 1
 for r in 64 128 256; do
   timeout -k 10 120 tools/fold_bench 64 $r 22 >> $out/sweep.jsonl || exit 1
