@@ -31,11 +31,19 @@
 #ifndef DPF_EVAL_BATCH
 #define DPF_EVAL_BATCH 1
 #endif
+#ifndef DPF_PRIO_STEPS
+#define DPF_PRIO_STEPS 3   // wave issue priority lowered by progress (prio_step)
+#endif
 #ifndef DPF_WALK_BATCH
 #define DPF_WALK_BATCH 1   // tree kernels' root-to-subtree walks: batched single-block rounds
 #endif
 
 namespace dpfk {
+
+#ifdef DPF_WAVE_TIMES
+constexpr uint64_t kWaveTimesMax = 1u << 16;
+__device__ uint64_t g_wave_times[4 * kWaveTimesMax];
+#endif
 
 struct Node {
     Blk s;
@@ -127,7 +135,37 @@ struct Ctx {
     uint8_t* outp;      // leaf mode: 16-byte leaf cursor
     uint4* nseed;       // node mode: seed cursor
     uint8_t* nt;        // node mode: t cursor
+    uint32_t groups;    // 4-leaf groups finished (wave priority steps, prio_step)
 };
+
+// Issue priority by progress.  A SIMD's waves issue oldest-first, so of the
+// 4 waves sharing one, the oldest finishes its subtree first and the
+// youngest runs alone at the end, when the CU's LDS idles (per-wave wall
+// clock, tools/wave_times.hip, configs[1]: the 4 slots of every SIMD end at
+// 455 / 635 / 825 / 1015 us; waves busy 71% of the kernel's span).  Waves
+// lower their priority as they pass progress thresholds (fractions of the
+// thread's 4-leaf groups), so waves that are ahead yield the issue slots to
+// the ones behind and a SIMD's waves finish close together (busy 95%;
+// kernel 1048 -> 948 us on one box, profiles/r03/prio/).
+//   DPF_PRIO_STEPS 3: thresholds 3/4, 7/8, 15/16 (default);
+//   2: 1/2, 3/4, 7/8;  1: 1/4, 1/2, 3/4;  0: off.
+template <int DMAX>
+__device__ __forceinline__ void prio_step(Ctx& c) {
+#if DPF_PRIO_STEPS
+    constexpr uint32_t total = DMAX >= 2 ? 1u << (DMAX - 2) : 1u;   // 4-leaf groups per thread
+    const uint32_t d = ++c.groups;
+    constexpr uint32_t den = DPF_PRIO_STEPS == 1 ? 4 : DPF_PRIO_STEPS == 2 ? 8 : 16;
+    constexpr uint32_t t1 = DPF_PRIO_STEPS == 1 ? 1 : DPF_PRIO_STEPS == 2 ? 4 : 12;
+    constexpr uint32_t t2 = DPF_PRIO_STEPS == 1 ? 2 : DPF_PRIO_STEPS == 2 ? 6 : 14;
+    constexpr uint32_t t3 = DPF_PRIO_STEPS == 1 ? 3 : DPF_PRIO_STEPS == 2 ? 7 : 15;
+    const uint32_t x = d * den;
+    if (x >= t3 * total) __builtin_amdgcn_s_setprio(0);
+    else if (x >= t2 * total) __builtin_amdgcn_s_setprio(1);
+    else if (x >= t1 * total) __builtin_amdgcn_s_setprio(2);
+#else
+    (void)c;
+#endif
+}
 
 __device__ __forceinline__ void emit_node(Ctx& c, const Node& n) {
     *c.nseed++ = make_uint4(n.s.c0, n.s.c1, n.s.c2, n.s.c3);
@@ -220,6 +258,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
 #pragma nounroll
         for (int h = 0; h < 2; ++h) {   // one code copy of leaves4 (instruction cache)
             leaves4<B>(c, lvl0 + DMAX - 2, cur, c.outp + (h == 0 ? (odd ? 64 - sub : 0) : (odd ? 64 : sub)));
+            prio_step<DMAX>(c);
             cur = second;
         }
         c.outp += 128;
@@ -235,6 +274,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         // Bottom two levels at once: 4 leaves = 64 contiguous bytes stored back
         // to back (subtrees too shallow or lanes of different keys for PAIR).
         leaves4<B>(c, lvl0 + DMAX - 2, n, c.outp);
+        prio_step<DMAX>(c);
         c.outp += 64;
     } else if constexpr (D == 2 && NODES) {
         // Bottom two levels of a frontier at once: 4 seeds = 64 contiguous
@@ -253,6 +293,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
                                              ((q[3].t & 0xffu) << 24);
         c.nseed += 4;
         c.nt += 4;
+        prio_step<DMAX>(c);
     } else if constexpr (D == 1) {
         CW cw = load_cw(c.ek, lvl0 + DMAX - 1);
         Node L, R;
@@ -319,6 +360,9 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
                                                         uint64_t nunits, uint32_t units_log, uint32_t ltop,
                                                         uint64_t sub_base, uint8_t* __restrict__ out,
                                                         uint8_t* __restrict__ out_t, uint64_t out_stride) {
+#ifdef DPF_WAVE_TIMES
+    const uint64_t t_start = wall_clock64();
+#endif
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
     fill_table(s_tab);
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kTreeBlock
@@ -330,6 +374,10 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     const uint32_t* ek = ekeys + key * ((uint64_t)(stop + 2) * 8);
 
     Ctx c;
+    c.groups = 0;
+#if DPF_PRIO_STEPS
+    __builtin_amdgcn_s_setprio(3);
+#endif
     c.tab = reinterpret_cast<const uint8_t*>(s_tab);
     c.lo = (threadIdx.x & 31u) * 4u;
     c.ek = ek;
@@ -384,6 +432,19 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     // stores for A/B runs.
     constexpr bool kPair = DPF_PAIR_STORES && UNIFORM && !NODES && D >= 3;
     dfs<D, D, NODES, kPair, UNIFORM>(c, ltop, n);
+#ifdef DPF_WAVE_TIMES
+    // Measurement build only (tools/wave_times.hip): per wave, start / end
+    // (wall clock) and the hardware ids of the CU it ran on.
+    if ((threadIdx.x & 63) == 0) {
+        const uint64_t wv = u >> 6;
+        if (wv < kWaveTimesMax) {
+            g_wave_times[4 * wv] = t_start;
+            g_wave_times[4 * wv + 1] = wall_clock64();
+            g_wave_times[4 * wv + 2] = __builtin_amdgcn_s_getreg(0xF804);   // HW_ID
+            g_wave_times[4 * wv + 3] = __builtin_amdgcn_s_getreg(0xF814);   // XCC_ID
+        }
+    }
+#endif
 }
 
 // Batched Eval: one thread per query, independent walks that compute only
