@@ -26,6 +26,10 @@
 #include "bs_kernels.hpp"
 #include "dpf_kernels.hpp"
 
+#ifndef DPF_BS_PRIO
+#define DPF_BS_PRIO 1   // issue priority by progress in k_evalfull_bs
+#endif
+
 namespace dpfk {
 
 using bs::aes_mmo8;
@@ -251,6 +255,13 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
     uint32_t S2[32];
     uint32_t tS0 = 0, tS1 = 0, tS2 = 0;
     uint32_t d = 0, path = 0;
+#if DPF_BS_PRIO
+    // Issue priority by progress, as the T-table tree kernel's prio_step:
+    // 3 until 3/4 of the lane's leaf-set pairs, 2, then 1 at 7/8.
+    uint32_t pairs = 0;
+    constexpr uint32_t kPairs = 1u << (D - 1);
+    __builtin_amdgcn_s_setprio(3);
+#endif
     for (;;) {
         const uint32_t* cw = ek + (uint64_t)(lvl0 + d) * kBsRec;
         uint32_t L[32], R[32], B[32];
@@ -290,6 +301,11 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
             aes_mmo8(B, O, 0);
             leaf_store(O, tB, fcw, obase + (uint64_t)(path + 1) * 128, sig);
         }
+#if DPF_BS_PRIO
+        ++pairs;
+        if (pairs * 8 >= 7 * kPairs) __builtin_amdgcn_s_setprio(1);
+        else if (pairs * 4 >= 3 * kPairs) __builtin_amdgcn_s_setprio(2);
+#endif
         path >>= 1;                               // back to X's own index at depth d
         while (d > 0 && (path & 1u)) {            // climb over finished right branches
             path >>= 1;

@@ -57,6 +57,22 @@ __device__ __forceinline__ void zero_answers(uint32_t* zero, uint64_t words) {
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x)
         zero[t] = 0;
 }
+// Issue priority by progress (as the tree kernels' prio_step): a SIMD's
+// waves issue oldest-first, so without it the oldest workgroup on a CU
+// finishes first and the youngest runs alone at the end.  Priority 3 until
+// 3/4 of the wave's range, then 2, 1 at 7/8, 0 at 15/16.
+__device__ __forceinline__ void fold_prio(uint64_t done, uint64_t all) {
+#if DPF_FOLD_PRIO
+    const uint64_t x = done * 16;
+    if (x >= 15 * all) __builtin_amdgcn_s_setprio(0);
+    else if (x >= 14 * all) __builtin_amdgcn_s_setprio(1);
+    else if (x >= 12 * all) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+#else
+    (void)done;
+    (void)all;
+#endif
+}
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -97,6 +113,9 @@ __device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool liv
 // wave takes every 4th chunk of the workgroup's contiguous range.  Lane l
 // always holds the same 16-byte position u = l mod 2C of its records, so its
 // accumulators are 4 words per key, XOR-reduced across lanes at the end.
+#ifndef DPF_FOLD_PRIO
+#define DPF_FOLD_PRIO 1   // issue priority by progress (fold_prio)
+#endif
 #ifndef DPF_FOLD_PIPE
 #define DPF_FOLD_PIPE 1   // table pairs in flight per wave in k_fold4r's lookups (2: no gain, fold_bench r03)
 #endif
@@ -176,6 +195,7 @@ __global__ __launch_bounds__(64 * kDWaves) void k_fold_direct(const uint32_t* __
         }
     };
     for (uint64_t cp = c0 + w; cp < cend; cp += 2 * kDWaves) {
+        fold_prio(cp - c0, cend - c0);
 #pragma unroll
         for (int i = 0; i < 2 * C; i += 2) {
             step(cp, i, A0, B0, S0, A1, B1, S1);
@@ -393,6 +413,7 @@ __global__ __launch_bounds__(64 * WV, WV == 8 ? 4 : 3) void k_fold4r(const uint3
         if (cc < cend) fold(cc, q, cb, A, B);
     };
     for (uint64_t cb = c0; cb < cend; cb += Cfg::batch) {
+        fold_prio(cb - c0, cend - c0);
         __syncthreads();                                   // previous batch's selection reads are done
 #pragma unroll
         for (int kg = 0; kg < KW; ++kg) {

@@ -8,7 +8,7 @@ REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$REPO"
 OUT="gpurun_out/$1"; WL="$2"; shift 2
 mkdir -p "$OUT"
-B=(--workload "$WL" --steps 30 --warmup 5 --spinup 0.5 --no-cpu-baseline --no-variants --no-api --no-sweep --aes ttable)
+B=(--workload "$WL" --steps 30 --warmup 5 --spinup 0.5 --no-cpu-baseline --no-variants --no-api --no-sweep --aes "${AES:-ttable}")
 lib() { if [ "$1" = base ]; then echo "$REPO/dpf-go_amd/lib/libdpf_hip.so"; else echo "$REPO/tools/bin/libdpf_hip_$1.so"; fi; }
 for r in 1 2 3; do
   for v in "$@"; do
