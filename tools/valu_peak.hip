@@ -62,7 +62,14 @@ __global__ __launch_bounds__(1024) void k_lds(uint32_t* out, uint32_t seed) {
     const uint32_t lo = (threadIdx.x & 63) * 4;
     uint32_t x[8];
     for (int j = 0; j < 8; ++j) x[j] = (seed + threadIdx.x * 8 + j) * 2654435761u;
+    // Issue priority by progress (dpf_kernels.hip prio_step): without it a
+    // SIMD's waves finish oldest-first and the tail of the one round runs on
+    // fewer waves (r01's 16.44 T lookups/s was measured that way).
+    __builtin_amdgcn_s_setprio(3);
     for (int i = 0; i < kIters; ++i) {
+        if (i == kIters * 3 / 4) __builtin_amdgcn_s_setprio(2);
+        if (i == kIters * 7 / 8) __builtin_amdgcn_s_setprio(1);
+        if (i == kIters * 15 / 16) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             uint32_t a = __builtin_amdgcn_perm(x[j], lo, 0x0c0c0500u);
