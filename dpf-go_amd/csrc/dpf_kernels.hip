@@ -28,6 +28,12 @@
 #ifndef DPF_MMO_INTERLEAVE
 #define DPF_MMO_INTERLEAVE 1
 #endif
+#ifndef DPF_EVAL_STRIDE
+#define DPF_EVAL_STRIDE 0   // 1: k_eval2 grid = resident workgroups only (slower: 3667 vs 3489 us)
+#endif
+#ifndef DPF_EVAL_PAIRS
+#define DPF_EVAL_PAIRS 1   // batched Eval: two queries per thread (k_eval2)
+#endif
 #ifndef DPF_EVAL_BATCH
 #define DPF_EVAL_BATCH 1
 #endif
@@ -105,16 +111,26 @@ __device__ __forceinline__ void expand(const uint8_t* tab, uint32_t lo, const No
 
 // One step of a root-to-node walk that computes only the child selected by
 // `bit` (dpf.go:183-201, minus the unused sibling).
-template <bool B = false>
-__device__ __forceinline__ void walk_step(const uint8_t* tab, uint32_t lo, Node& n, const CW& cw, uint32_t bit) {
-    uint32_t kb = bit ? 0xffffffffu : 0u;
-    Blk c = mmo1<B>(tab, lo, KeySel{kb}, n.s);
+__device__ __forceinline__ void walk_fix(Node& n, Blk c, const CW& cw, uint32_t bit) {
     uint32_t tc = c.c0 & 1u;
     c.c0 &= ~1u;
     uint32_t m = tmask(n.t);
     c.c0 ^= m & cw.s.c0; c.c1 ^= m & cw.s.c1; c.c2 ^= m & cw.s.c2; c.c3 ^= m & cw.s.c3;
     n.s = c;
     n.t = tc ^ (m & (bit ? cw.tr : cw.tl));
+}
+template <bool B = false>
+__device__ __forceinline__ void walk_step(const uint8_t* tab, uint32_t lo, Node& n, const CW& cw, uint32_t bit) {
+    walk_fix(n, mmo1<B>(tab, lo, KeySel{bit ? 0xffffffffu : 0u}, n.s), cw, bit);
+}
+// Two independent walks advanced together (two queries per thread).
+template <bool B = false>
+__device__ __forceinline__ void walk_step2(const uint8_t* tab, uint32_t lo, Node& n0, const CW& cw0, uint32_t bit0,
+                                           Node& n1, const CW& cw1, uint32_t bit1) {
+    Blk c0, c1;
+    mmo2<B>(tab, lo, KeySel{bit0 ? 0xffffffffu : 0u}, n0.s, c0, KeySel{bit1 ? 0xffffffffu : 0u}, n1.s, c1);
+    walk_fix(n0, c0, cw0, bit0);
+    walk_fix(n1, c1, cw1, bit1);
 }
 
 __device__ __forceinline__ void store16(uint8_t* p, Blk v) {
@@ -489,6 +505,81 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     out[q] = (uint8_t)((w >> (b & 31)) & 1u);
 }
 
+// Batched Eval, two queries per thread (q = 2u, 2u + 1): the two walks run
+// in lockstep (same start level and length), so every AES round issues 32
+// lookups per wave instead of 16.  Same output as k_eval.
+__device__ __forceinline__ Node eval_start(const uint32_t* ek, uint64_t key, uint64_t x, uint32_t logN,
+                                           const uint4* fseed, const uint8_t* ft, uint32_t L) {
+    Node n;
+    if (fseed != nullptr) {
+        const uint64_t idx = (key << L) + ((x >> (logN - L)) & ((1ull << L) - 1));
+        const uint4 v = fseed[idx];
+        n.s = {v.x, v.y, v.z, v.w};
+        n.t = ft[idx];
+    } else {
+        n.s = load_blk(ek);
+        n.t = ek[4];
+    }
+    return n;
+}
+__device__ __forceinline__ uint8_t eval_bit(Blk o, uint64_t x) {
+    const uint32_t b = (uint32_t)(x & 127);
+    const uint32_t w = (b >> 5) == 0 ? o.c0 : (b >> 5) == 1 ? o.c1 : (b >> 5) == 2 ? o.c2 : o.c3;
+    return (uint8_t)((w >> (b & 31)) & 1u);
+}
+__device__ __forceinline__ void eval_pair(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
+                                          const uint64_t* __restrict__ xs, uint64_t nq, uint64_t pts_per_key,
+                                          const uint4* __restrict__ fseed, const uint8_t* __restrict__ ft, uint32_t L,
+                                          uint8_t* __restrict__ out, const uint32_t* s_tab, uint64_t q0) {
+    const bool two = q0 + 1 < nq;
+    const uint64_t q1 = two ? q0 + 1 : q0;
+    const uint64_t key0 = q0 / pts_per_key, key1 = q1 / pts_per_key;
+    const uint64_t rec = (uint64_t)(stop + 2) * 8;
+    const uint32_t* ek0 = ekeys + key0 * rec;
+    const uint32_t* ek1 = ekeys + key1 * rec;
+    const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
+    const uint32_t lo = (threadIdx.x & 31u) * 4u;
+    const uint64_t x0 = xs[q0], x1 = xs[q1];
+    Node n0 = eval_start(ek0, key0, x0, logN, fseed, ft, L);
+    Node n1 = eval_start(ek1, key1, x1, logN, fseed, ft, L);
+    for (uint32_t i = fseed != nullptr ? L : 0; i < stop; ++i) {
+        const CW cw0 = load_cw(ek0, i), cw1 = load_cw(ek1, i);
+        walk_step2<DPF_EVAL_BATCH>(tab, lo, n0, cw0, (uint32_t)(x0 >> (logN - 1 - i)) & 1u, n1, cw1,
+                                   (uint32_t)(x1 >> (logN - 1 - i)) & 1u);
+    }
+    Blk o0, o1;
+    mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n0.s, o0, KeyFixed<false>{}, n1.s, o1);
+    o0 = leaf_fix(o0, n0.t, load_blk(ek0 + 8 + 8 * stop));
+    o1 = leaf_fix(o1, n1.t, load_blk(ek1 + 8 + 8 * stop));
+    out[q0] = eval_bit(o0, x0);
+    if (two) out[q1] = eval_bit(o1, x1);
+}
+
+__global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict__ ekeys, uint32_t stop,
+                                                     uint32_t logN, const uint64_t* __restrict__ xs, uint64_t nq,
+                                                     uint64_t pts_per_key, const uint4* __restrict__ fseed,
+                                                     const uint8_t* __restrict__ ft, uint32_t L,
+                                                     uint8_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+    fill_table(s_tab);
+    // Grid-stride loop.  launch_eval launches one thread per query pair
+    // (iters = 1); DPF_EVAL_STRIDE=1 caps the grid at the resident
+    // workgroups so each fills its 64 KiB table once, with the issue priority
+    // stepped down by progress like the tree kernels -- measured slower
+    // (3667 vs 3489 us at configs[2]): a thread's frontier gathers are then
+    // serialised, where short-lived waves overlap them.
+    const uint64_t stride = 2 * (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t first = 2 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    const uint64_t iters = first < nq ? (nq - first + stride - 1) / stride : 0;
+    __builtin_amdgcn_s_setprio(3);
+    for (uint64_t it = 0; it < iters; ++it) {
+        if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
+        else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
+        else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
+        eval_pair(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, out, s_tab, first + it * stride);
+    }
+}
+
 // aes128MMO microbenchmark / self-test on the T-table back end: two
 // independent blocks per thread (the PRG's own ILP), iterated `reps` times.
 template <bool RIGHT>
@@ -684,10 +775,22 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
         fseed = reinterpret_cast<const uint4*>(fs);
         ft = fts;
     }
+#if DPF_EVAL_PAIRS
+    const uint64_t nthreads = (nq + 1) / 2;
+    const uint32_t block = pick_block(nthreads, kBlock);
+    uint64_t blocks = (nthreads + block - 1) / block;
+    // Resident workgroups only (64 KiB of table each: 2 per CU); k_eval2
+    // strides over the rest.
+    const uint64_t resident = 2 * (uint64_t)cu_count();
+    if (DPF_EVAL_STRIDE && blocks > resident) blocks = resident;
+    hipLaunchKernelGGL(k_eval2, dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop, logN, xs, nq, pts_per_key,
+                       fseed, ft, L, out);
+#else
     const uint32_t block = pick_block(nq, kBlock);
     const uint64_t blocks = (nq + block - 1) / block;
     hipLaunchKernelGGL(k_eval, dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop, logN, xs, nq, pts_per_key,
                        fseed, ft, L, out);
+#endif
     return hipGetLastError();
 }
 
