@@ -221,7 +221,7 @@ def test_logN32_single_key_property():
 
 
 @pytest.mark.parametrize("logN,nk,ppk", [(13, 8, 256), (14, 5, 1000), (20, 6, 1024), (20, 3, 3000), (32, 4, 512),
-                                         (63, 2, 700)])
+                                         (63, 2, 700), (15, 3, 257)])
 def test_eval_frontier_path_vs_oracle(logN, nk, ppk):
     """Shared-frontier Eval kernel (taken when a key has >= 256 points)."""
     _, ka, _ = _keys(nk, logN, first=8000 + logN + ppk)
@@ -232,6 +232,15 @@ def test_eval_frontier_path_vs_oracle(logN, nk, ppk):
     got = dpf.eval_batch(ka, xs, logN, ngpus=1)
     want = oracle.eval_batch(ka, xs, logN, nthreads=NT)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("logN,nk,ppk", [(10, 5, 7), (20, 1, 1), (9, 3, 33)])
+def test_eval_odd_query_counts(logN, nk, ppk):
+    """k_eval2 takes queries in pairs: odd totals and pairs that straddle two
+    keys (odd points per key) must match the oracle too."""
+    _, ka, _ = _keys(nk, logN, first=8100 + logN + ppk)
+    xs = synth.eval_points(nk, ppk, logN)
+    assert np.array_equal(dpf.eval_batch(ka, xs, logN, ngpus=1), oracle.eval_batch(ka, xs, logN, nthreads=NT))
 
 
 def test_empty_and_degenerate_inputs():
