@@ -32,10 +32,16 @@
 //                  ds_read_b128 per key per group instead of 32 masked XORs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "pir_kernels.hpp"
 
 namespace dpfk {
+
+#ifdef DPF_FOLD_TIMES
+constexpr uint64_t kFoldTimesMax = 1u << 14;
+__device__ uint64_t g_fold_times[4 * kFoldTimesMax];
+#endif
 
 // v_bitop3_b32 truth tables: src0 = 0xF0, src1 = 0xCC, src2 = 0xAA.
 constexpr uint8_t kTT0 = 0xF0, kTT1 = 0xCC, kTT2 = 0xAA;
@@ -115,6 +121,9 @@ __device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool liv
 // accumulators are 4 words per key, XOR-reduced across lanes at the end.
 #ifndef DPF_FOLD_PRIO
 #define DPF_FOLD_PRIO 1   // issue priority by progress (fold_prio)
+#endif
+#ifndef DPF_FOLD_SKEW_DEFAULT
+#define DPF_FOLD_SKEW_DEFAULT 62   // percent of a CU's chunk pair for its first k_fold4r workgroup (launch_4r)
 #endif
 #ifndef DPF_FOLD_PIPE
 #define DPF_FOLD_PIPE 1   // table pairs in flight per wave in k_fold4r's lookups (2: no gain, fold_bench r03)
@@ -268,7 +277,8 @@ __global__ __launch_bounds__(64 * WV, WV == 8 ? 4 : 3) void k_fold4r(const uint3
                                                                     uint64_t rec_u4, uint32_t col, uint32_t nkeys,
                                                                     uint64_t chunks_per_block,
                                                                     uint32_t* __restrict__ parts,
-                                                                    uint32_t* __restrict__ zero, uint64_t zero_words) {
+                                                                    uint32_t* __restrict__ zero, uint64_t zero_words,
+                                                                    uint32_t nfirst, uint64_t cpb_first) {
     zero_answers(zero, zero_words);
     using Cfg = Fold4rCfg<WV>;
     __shared__ uint4 s_tab[WV][32 * 16];                                   // 8 KiB per wave
@@ -276,9 +286,16 @@ __global__ __launch_bounds__(64 * WV, WV == 8 ? 4 : 3) void k_fold4r(const uint3
     const uint32_t l = threadIdx.x & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nchunks = (nrec + 63) / 64;
-    const uint64_t c0 = (uint64_t)blockIdx.x * chunks_per_block;
-    const uint64_t cend = c0 + chunks_per_block < nchunks ? c0 + chunks_per_block : nchunks;
+    // The first nfirst workgroups (dispatched first: one per CU) take
+    // cpb_first chunks, the rest chunks_per_block (fold_split below).
+    const uint64_t b = blockIdx.x;
+    const uint64_t c0 = b < nfirst ? b * cpb_first : nfirst * cpb_first + (b - nfirst) * chunks_per_block;
+    const uint64_t my = b < nfirst ? cpb_first : chunks_per_block;
+    const uint64_t cend = c0 + my < nchunks ? c0 + my : nchunks;
     uint4* tab = s_tab[w];
+#ifdef DPF_FOLD_TIMES
+    const uint64_t t_start = wall_clock64();
+#endif
 
     // Entry 0 of every row: a zero slot, written once.
     if (l < 32) tab[l * 16 + sw_row(l >> 1, l & 1)] = make_uint4(0, 0, 0, 0);
@@ -430,6 +447,19 @@ __global__ __launch_bounds__(64 * WV, WV == 8 ? 4 : 3) void k_fold4r(const uint3
             step(cb, i + 1, A1, B1, A0, B0);
         }
     }
+#ifdef DPF_FOLD_TIMES
+    // Measurement build only (tools/fold_bench.hip -DDPF_FOLD_TIMES): per
+    // wave, start / end of its chunk loop and the CU it ran on.
+    if (l == 0) {
+        const uint64_t wv = (uint64_t)blockIdx.x * WV + w;
+        if (wv < kFoldTimesMax) {
+            g_fold_times[4 * wv] = t_start;
+            g_fold_times[4 * wv + 1] = wall_clock64();
+            g_fold_times[4 * wv + 2] = __builtin_amdgcn_s_getreg(0xF804);   // HW_ID
+            g_fold_times[4 * wv + 3] = __builtin_amdgcn_s_getreg(0xF814);   // XCC_ID
+        }
+    }
+#endif
     // Combine the workgroup's waves in LDS (reusing the tables), one
     // 8-word slice (key group, column) at a time: parts[block][key][8C words].
     constexpr uint32_t pkeys = 64 * KW, pwords = 8 * C;
@@ -523,11 +553,34 @@ hipError_t launch_4r(const FoldArgs& a, uint64_t nchunks, uint64_t& blocks, hipS
     // VGPRs) per CU.  Otherwise 4 waves, 41-50 KiB -> 3 per CU (168 VGPRs:
     // 64 accumulators per lane).
     constexpr int WV = KW == 1 && C < 8 ? 8 : 4;
+    const uint64_t cus = (uint64_t)cu_count_fold();
     const uint64_t per_cu = WV == 8 ? 2 : 3;
     uint64_t cpb;
-    split_chunks(nchunks, (uint64_t)cu_count_fold() * per_cu, 2 * WV, blocks, cpb);
+    split_chunks(nchunks, cus * per_cu, 2 * WV, blocks, cpb);
+    // Two workgroups per CU: a SIMD's waves issue oldest-first, so the CU's
+    // first workgroup runs ahead of its second (fold per-wave times: 100 vs
+    // 143 us at configs[4]).  DPF_FOLD_SKEW (percent of a CU pair's chunks
+    // for the first workgroup) shifts work to it.
+    static const int skew = [] {
+        const char* e = getenv("DPF_FOLD_SKEW");
+        return e ? atoi(e) : DPF_FOLD_SKEW_DEFAULT;
+    }();
+    uint32_t nfirst = 0;
+    uint64_t cpb_first = cpb;
+    const uint64_t gran = 2 * WV;
+    if (per_cu == 2 && skew > 50 && skew < 100 && blocks == 2 * cus) {
+        const uint64_t pair = 2 * cpb;
+        cpb_first = (pair * (uint64_t)skew / 100 + gran / 2) / gran * gran;
+        const uint64_t rest = pair - cpb_first;
+        if (rest >= gran && nchunks <= cus * pair) {
+            nfirst = (uint32_t)cus;
+            cpb = rest;
+        } else {
+            cpb_first = cpb;
+        }
+    }
     hipLaunchKernelGGL((k_fold4r<C, KW, WV>), dim3((uint32_t)blocks), dim3(64 * WV), 0, st, a.bits, a.wpk, a.db,
-                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts, a.zero, a.zero_words);
+                       a.nrec, a.rec_u4, a.col, a.nkeys, cpb, a.parts, a.zero, a.zero_words, nfirst, cpb_first);
     return hipGetLastError();
 }
 

@@ -85,5 +85,24 @@ int main(int argc, char** argv) {
            FOLD_SRC, nkeys, (unsigned long long)rec_bytes, (unsigned long long)nrec, p.direct ? "direct" : "4r", p.kw,
            p.col_passes, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
            p.col_passes * ((nkeys + p.keys_per_pass - 1) / p.keys_per_pass), bad ? "false" : "true");
+#ifdef DPF_FOLD_TIMES
+    {   // per-wave start / end of the last launch (k_fold4r only)
+        std::vector<uint64_t> t(4 * dpfk::kFoldTimesMax);
+        CK(hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(dpfk::g_fold_times), t.size() * 8));
+        int rate_khz = 0;
+        CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
+        uint64_t t0 = ~0ull;
+        for (size_t w = 0; w < dpfk::kFoldTimesMax; ++w)
+            if (t[4 * w + 1]) t0 = t[4 * w] < t0 ? t[4 * w] : t0;
+        FILE* f = fopen(getenv("FOLD_TIMES_CSV") ? getenv("FOLD_TIMES_CSV") : "fold_times.csv", "w");
+        fprintf(f, "wave,start_us,end_us,hw_id,xcc_id\n");
+        for (size_t w = 0; w < dpfk::kFoldTimesMax; ++w)
+            if (t[4 * w + 1])
+                fprintf(f, "%zu,%.3f,%.3f,%llu,%llu\n", w, (t[4 * w] - t0) * 1e3 / rate_khz,
+                        (t[4 * w + 1] - t0) * 1e3 / rate_khz, (unsigned long long)t[4 * w + 2],
+                        (unsigned long long)t[4 * w + 3]);
+        fclose(f);
+    }
+#endif
     return bad ? 1 : 0;
 }
