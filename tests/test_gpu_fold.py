@@ -72,6 +72,20 @@ def test_xor_fold_matches_oracle(logN, nk, rec_bytes, nrec):
     assert np.array_equal(got, _want(full, payload, nrec))
 
 
+@pytest.mark.parametrize("nk,nrec", [(64, 1 << 19), (40, (1 << 19) - 1000), (64, (1 << 19) + 4321)])
+def test_xor_fold_full_grid_vs_numpy(nk, nrec):
+    """A grid of 2 workgroups per CU, where launch_4r splits a CU's chunks
+    unevenly between them (DPF_FOLD_SKEW): every record must be folded once.
+    Random selection bits, checked against a numpy fold of all keys."""
+    import torch
+    rng = np.random.default_rng(nk + nrec)
+    stride = ((nrec + 127) // 128) * 16
+    bits = rng.integers(0, 256, size=(nk, stride), dtype=np.uint8)
+    payload = rng.integers(0, 256, size=(nrec, 32), dtype=np.uint8)
+    got = _fold(torch.from_numpy(bits.reshape(-1)).cuda(), stride, nk, payload, nrec, 32)
+    assert np.array_equal(got, _want(bits, payload, nrec))
+
+
 def test_xor_fold_two_server_property_logN20():
     """answer(ka) ^ answer(kb) == payload[alpha] for 128-byte records at logN=20."""
     import torch
