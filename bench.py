@@ -222,6 +222,61 @@ def cpu_baseline(logN: int, target_s: float = 10.0) -> dict:
                       f"{cores} threads, AES-NI one block per call; oracle/dpf_oracle.c)"}
 
 
+def cpu_baseline_eval(logN: int, nkeys: int, ppk: int, target_s: float = 8.0) -> dict:
+    """configs[2] on the host: the oracle's reference-faithful Eval (AES-NI,
+    both children per level like dpf.go:171-211) over a bounded sample of
+    keys x points, one key's points per thread at a time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from dpf import synth
+    import dpf
+    cores = host_cpus()["use"]
+    nk = min(nkeys, cores * 4)
+    al, s0, s1 = synth.key_seeds(nk, logN)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    xs = synth.eval_points(nk, ppk, logN)
+    oracle.eval_batch(ka[:1], xs[:1], logN, nthreads=1)
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        oracle.eval_batch(ka, xs, logN, nthreads=cores)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= target_s:
+            break
+    q = passes * nk * ppk
+    return {"value": q / dt, "unit": "queries/s", "cores": cores, "kind": "port",
+            "sample": f"{passes} passes over {nk} keys x {ppk} points at logN={logN} ({dt:.1f} s, {cores} "
+                      f"threads; oracle/dpf_oracle.c Eval, AES-NI one block per call)"}
+
+
+def cpu_baseline_pir(logN: int, batch: int, target_s: float = 8.0) -> dict:
+    """configs[4] on the host: the oracle's PIR answer (AES-NI EvalFull of
+    the key, then a byte-wise XOR fold of the selected 32-B records), one
+    query per thread, over a bounded number of queries."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from dpf import synth
+    import dpf
+    from concurrent.futures import ThreadPoolExecutor
+    cores = host_cpus()["use"]
+    nrec = 1 << logN
+    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    al, s0, s1 = synth.key_seeds(max(batch, cores), logN, first=4242)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    keys = [k.tobytes() for k in ka]
+    done, t0 = 0, time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:       # ctypes releases the GIL during each answer
+        while True:
+            list(ex.map(lambda k: oracle.pir_answer(k, logN, db, 0, nrec), keys[:cores]))
+            done += cores
+            dt = time.perf_counter() - t0
+            if dt >= target_s:
+                break
+    return {"value": done / dt, "unit": "queries/s", "cores": cores, "kind": "port",
+            "sample": f"{done} PIR answers at logN={logN} over a {nrec}-record x 32-B DB ({dt:.1f} s, {cores} "
+                      f"threads; oracle/dpf_oracle.c oracle_pir_answer)"}
+
+
 class Ctx:
     def __init__(self, args):
         import torch
@@ -764,8 +819,18 @@ def finalize(line: dict, args, world: int, folded: bool) -> None:
     baseline at every N (taken after the timed steps, so it cannot perturb
     them).  Ranks folded onto fewer GPUs than ranks are a rehearsal of the
     N-rank plumbing, not an N-GPU number: marked, and no scaling class."""
-    if args.workload == "evalfull" and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.logN, args.cpu_seconds)
+    if not args.no_cpu_baseline:
+        if args.workload == "evalfull":
+            line["cpu_baseline"] = cpu_baseline(args.logN, args.cpu_seconds)
+        elif args.workload == "split":
+            line["cpu_baseline"] = cpu_baseline(20, min(args.cpu_seconds, 8.0))
+            line["cpu_baseline"]["note"] = ("points/s of the batched EvalFull port at logN=20: the per-point "
+                                            "rate of a logN=32 EvalFull on the same code")
+        elif args.workload == "eval":
+            line["cpu_baseline"] = cpu_baseline_eval(args.logN, args.eval_keys, args.eval_points,
+                                                     min(args.cpu_seconds, 8.0))
+        elif args.workload == "pir":
+            line["cpu_baseline"] = cpu_baseline_pir(args.pir_logN, args.batch, min(args.cpu_seconds, 8.0))
     if folded:
         line["folded_ranks"] = True
         line["scaling"] = None
