@@ -115,7 +115,8 @@ def test_bench_gpus_flag_spawns_ranks():
     assert "roofline" in d
     p = run("--workload", "pir")
     assert p["roofline"]["traffic"] is None and "traffic_note" in p["roofline"]
-    assert "cpu_baseline" not in p
+    # ... and every workload line carries its own CPU baseline (queries/s here).
+    assert p["cpu_baseline"]["unit"] == "queries/s" and p["cpu_baseline"]["value"] > 0
 
 
 def test_xor_rows_matches_numpy():
