@@ -124,7 +124,7 @@ def test_xor_rows_matches_numpy():
     on CPU tensors: 8-byte lanes and the byte fallback."""
     import torch
     rng = np.random.default_rng(5)
-    for shape in ((8, 64, 32), (2, 5, 3), (1, 16)):
+    for shape in ((8, 64, 32), (2, 5, 3), (1, 16), (3, 8, 4), (7, 2, 8), (5, 9)):
         a = rng.integers(0, 256, shape, dtype=np.uint8)
         got = shard.xor_rows(torch.from_numpy(a)).numpy()
         assert got.shape == a.shape[1:]
