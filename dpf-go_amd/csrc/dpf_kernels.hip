@@ -40,6 +40,9 @@
 #ifndef DPF_PRIO_STEPS
 #define DPF_PRIO_STEPS 3   // wave issue priority lowered by progress (prio_step)
 #endif
+#ifndef DPF_DEPTH_MODEL_COOP
+#define DPF_DEPTH_MODEL_COOP 1   // pick_shape prices the shared walk (latency once + W - 6 per thread)
+#endif
 #ifndef DPF_WALK_BATCH
 #define DPF_WALK_BATCH 1   // tree kernels' root-to-subtree walks: batched single-block rounds
 #endif
@@ -668,7 +671,7 @@ static uint32_t pick_block(uint64_t n, uint32_t maxb) {
 struct TreeShape {
     uint32_t d, block;
 };
-static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes) {
+static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes, uint32_t prefix_bits) {
     static const int forced = [] {
         const char* e = getenv("DPF_SUBTREE_DEPTH");
         return e ? atoi(e) : -1;
@@ -686,11 +689,25 @@ static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes) {
     double best_t = 1e30;
     for (int dd = (int)dmax; dd >= 0; --dd) {
         const uint32_t d = (uint32_t)dd;
-        const double work = (double)(span - d) + (nodes ? 2.0 : 3.0) * (double)(1u << d) - 2.0;   // NODES: no leaf AES
+        double walk = (double)(span - d), lat = 0.0;
         const double w = (double)threads(d) / wave_slots;                 // waves per CU
         const double rounds = w > 16.0 ? std::ceil(w / 16.0) : 1.0;
         const double per = w > 16.0 ? 16.0 * kPerWave : std::max(kLat, w * kPerWave);
-        const double t = rounds * work * std::max(kLat, per);
+#if DPF_DEPTH_MODEL_COOP
+        // The shared workgroup walk (k_evalfull, DPF_COOP_WALK): one wave walks
+        // the top ltop - W + 6 levels alone (latency, once per round of
+        // workgroups), every thread the last W - 6.
+        const uint32_t bl = pick_block(threads(d), kTreeBlock);
+        const uint32_t W = 31u - (uint32_t)__builtin_clz(bl);
+        if (DPF_COOP_WALK && span - d >= 6 && (bl & (bl - 1)) == 0 && W >= 7 && span - d >= W) {
+            walk = (double)(W - 6);
+            lat = (double)(span + prefix_bits - d - W + 6) * kLat;
+        }
+#else
+        (void)prefix_bits;
+#endif
+        const double work = walk + (nodes ? 2.0 : 3.0) * (double)(1u << d) - 2.0;   // NODES: no leaf AES
+        const double t = rounds * (lat + work * std::max(kLat, per));
         if (t < best_t * 0.98) {          // prefer the deeper subtree on near-ties (less total work)
             best_t = t;
             best = d;
@@ -706,7 +723,7 @@ static hipError_t launch_tree(const uint32_t* ek, uint64_t nkeys, uint32_t stop,
                               uint32_t prefix_bits, uint64_t prefix, uint8_t* out, uint8_t* out_t,
                               uint64_t out_stride, hipStream_t st) {
     const uint32_t span = depth - prefix_bits;          // levels below the prefix node
-    const TreeShape sh = pick_shape(span, nkeys, NODES);
+    const TreeShape sh = pick_shape(span, nkeys, NODES, prefix_bits);
     const uint32_t d = sh.d;                             // per-thread subtree depth
     const uint32_t ltop = depth - d;                     // levels walked per thread
     const uint32_t units_log = ltop - prefix_bits;       // threads per key = 2^units_log
