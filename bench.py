@@ -77,37 +77,39 @@ def load_peaks() -> dict:
 
 def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, aes_impl: str = "lds-ttable",
                  workload: str = "evalfull", profiled_shape: bool = True) -> dict:
-    """PRG roofline: 22,928 two-input gate-equivalents per
-    AES-MMO block against the guide's VALU issue rate x 32 bit-lanes x 2
-    gates per v_bitop3 (5.03 P gate-eq/s).  `lds` is the T-table back end's
-    own ceiling: 160 ds_read_b32 lookups per block against the guide's
-    ~75 TB/s of ds_read_b32 (18.75 T lookups/s)."""
+    """Roofline of the PRG-bound kernels, named by the resource that binds.
+
+    T-table back end (the default): LDS.  Each AES-MMO block is 160
+    ds_read_b32 lookups (16 per round x 10), and the lookups, not the VALU,
+    bind (the LDS array is ~90% busy, VALU ~54%): achieved =
+    lookups/s against the guide's ~75 TB/s of ds_read_b32 = 18.75 T
+    lookups/s.  Byte-sliced back end: VALU.  Either way "gate" carries SURVEY
+    §8d's headline denominator beside it: 22,928 two-input gate-equivalents
+    per block against the guide's VALU issue rate x 32 bit-lanes x 2 gates per
+    v_bitop3 (5.03 P gate-eq/s)."""
     peaks = load_peaks()
-    achieved = aes_rate * GATES_PER_AES / 1e12
+    gate = aes_rate * GATES_PER_AES / 1e12
     gbs = hbm_bytes / (k_ms * 1e-3) / 1e9
-    r = {
-        "bound": "valu",
-        "achieved": round(achieved, 1),
-        "peak": round(GUIDE_GATE_PEAK_T, 1),
-        "unit": "Tgate/s (2-input gate-equivalents; 22,928 per AES-128-MMO block)",
-        "frac": round(achieved / GUIDE_GATE_PEAK_T, 4),
-        "traffic": None,
-        "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.64 T lane-op/s x 32 x 2",
-        "peak_measured": round(peaks["bitop3_Tops"] * 64, 1),
-        "frac_vs_measured": round(achieved / (peaks["bitop3_Tops"] * 64), 4),
-        "kernel": kernel,
-        "kernel_ms": round(k_ms, 4),
-        "aes_impl": aes_impl,
-        "aes_blocks_per_s": aes_rate,
-        "hbm_GBs": round(gbs, 1),
-        "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
-    }
+    gate_obj = {"bound": "valu", "achieved": round(gate, 1), "peak": round(GUIDE_GATE_PEAK_T, 1),
+                "unit": "Tgate/s (2-input gate-equivalents; 22,928 per AES-128-MMO block)",
+                "frac": round(gate / GUIDE_GATE_PEAK_T, 4),
+                "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.64 T lane-op/s x 32 x 2",
+                "peak_measured": round(peaks["bitop3_Tops"] * 64, 1),
+                "frac_vs_measured": round(gate / (peaks["bitop3_Tops"] * 64), 4)}
     if aes_impl == "lds-ttable":
         lk = aes_rate * LOOKUPS_PER_AES / 1e12
-        r["lds"] = {"bound": "lds", "achieved": round(lk, 3), "peak": GUIDE_LDS_LOOKUPS_T,
-                    "unit": "T lookups/s (ds_read_b32, 160 per AES-MMO block)",
-                    "frac": round(lk / GUIDE_LDS_LOOKUPS_T, 4),
-                    "peak_measured": round(peaks["lds_lookups_Gs"] / 1e3, 3)}
+        r = {"bound": "lds", "achieved": round(lk, 3), "peak": GUIDE_LDS_LOOKUPS_T,
+             "unit": "T lookups/s (ds_read_b32, 160 per AES-MMO block)",
+             "frac": round(lk / GUIDE_LDS_LOOKUPS_T, 4), "traffic": None,
+             "peak_source": "MI355X_MICROARCH.md: ds_read_b32 aggregate ~75 TB/s / 4 B",
+             "peak_measured": round(peaks["lds_lookups_Gs"] / 1e3, 3),
+             "frac_vs_measured": round(lk / (peaks["lds_lookups_Gs"] / 1e3), 4),
+             "gate": gate_obj}
+    else:
+        r = dict(gate_obj)
+        r["traffic"] = None
+    r.update({"kernel": kernel, "kernel_ms": round(k_ms, 4), "aes_impl": aes_impl, "aes_blocks_per_s": aes_rate,
+              "hbm_GBs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)})
     # Measured HBM bytes per launch of this kernel from the committed PMC
     # passes (tools/counters.sh + tools/traffic.py -> profiles/*traffic.json).
     # Multi-kernel steps (eval, pir) sum every dpf kernel of their own PMC
@@ -125,7 +127,8 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
                     t = json.load(f)
             except Exception:
                 continue
-            ks = sorted(k for k in t if k.startswith("k_"))
+            # PIR: the roofline is the tree's (k_unpack + k_evalfull); the fold has its own.
+            ks = sorted(k for k in t if k.startswith("k_") and (workload != "pir" or not k.startswith(("k_fold", "k_xor"))))
             tot = sum(t[k]["traffic_bytes"] for k in ks)
             r["traffic"] = round(tot)
             r["traffic_over_algorithmic"] = round(tot / hbm_bytes, 3)
@@ -369,10 +372,12 @@ def wl_evalfull(c: Ctx) -> dict:
     a, dpf, torch = c.args, c.dpf, c.torch
     from dpf import synth, shard
     logN = a.logN
+    W = c.world if c.world > 1 else max(1, a.emulate_world)
     if a.strong:
         # SURVEY 8d's strong-scaling form: a fixed batch of a.nkeys keys split
-        # over the ranks by range (no collective).
-        lo, hi = shard.key_range(a.nkeys, c.world, c.rank)
+        # over the ranks by range (no collective).  With --emulate-world W on
+        # one GPU: rank 0's share of a W-way split, timed alone.
+        lo, hi = shard.key_range(a.nkeys, W, c.rank)
         nk, first = hi - lo, lo
     else:
         nk, first = a.nkeys, c.rank * a.nkeys                        # weak: this rank's own batch
@@ -415,16 +420,22 @@ def wl_evalfull(c: Ctx) -> dict:
                                   "aes_blocks_per_s": aes / (k2 * 1e-3),
                                   "points_per_s": nk * (1 << logN) / (t2 / max(5, a.steps // 2)),
                                   "bit_identical_first_64_keys": bool(torch.equal(ref, d_out.view(nk, olen)[:64]))}
-    total = a.nkeys if a.strong else nk * c.world
+    emulated = a.strong and W != c.world
+    total = nk if emulated else a.nkeys if a.strong else nk * c.world
     line = c.line(metric=METRIC, value=total * (1 << logN) / sec, unit="points/s",
                   ms_per_step=sec * 1e3, scaling="strong" if a.strong else "weak",
                   data="synthetic (SplitMix64 seed 0x5EEDD9F0 keys via host Gen)",
-                  config={"workload": (f"batched EvalFull, {a.nkeys} keys x logN={logN} split over {c.world} GPU(s)"
+                  config={"workload": (f"batched EvalFull, {a.nkeys} keys x logN={logN} split over {W} GPU(s)"
+                                       + (f" (rank 0's {nk} keys timed on 1 GPU)" if emulated else "")
                                        if a.strong else
                                        f"batched EvalFull, {nk} keys x logN={logN} per GPU") + " (BASELINE configs[1])",
                           "keys_per_gpu": nk, "logN": logN, "aes": names[main_impl],
                           "parallelism": f"key-shard x{c.world}"},
                   aes_blocks_per_s=total * aes_full(logN) / sec)
+    if emulated:
+        line["emulated_world"] = {"world": W, "keys_per_rank": nk,
+                                  "implied_points_per_s": a.nkeys * (1 << logN) / sec,
+                                  "note": "if every rank ran rank 0's step time; not an N-GPU measurement"}
     kern = (f"k_evalfull<{min(stop_of(logN), 7)}, true, false>" if main_impl == dpf.AES_TTABLE
             else "k_evalfull<NODES>+k_evalfull_bs<true>")
     line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), kern, k_ms, nk * olen + nk * (stop_of(logN) + 2) * 32,
@@ -675,6 +686,55 @@ def pir_time(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int, warmup
     return ka, result, t_wall, k_ms
 
 
+def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -> dict:
+    """A PIR step's two phases timed apart with HIP events on the launch
+    stream: the tree (key unpack + subtree EvalFull into the selection bits:
+    dpf_evalfull_subtree_dev, what dpf_pir_answer_dev runs first) and the XOR
+    fold of the DB slice under those bits (dpf_xor_fold_dev: the same
+    launch_pir_fold call, its second half)."""
+    dpf, torch = c.dpf, c.torch
+    from dpf import synth, shard
+    logN = c.args.pir_logN
+    pb, prefix = shard.subtree_split(W, c.rank)
+    kl = dpf.key_len(logN)
+    per_key = dpf.evalfull_len(logN) >> pb
+    al, s0, s1 = synth.key_seeds(nk, logN, first=4242)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
+    d_bits = torch.empty(nk * per_key, dtype=torch.uint8, device=c.dev)
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=c.dev)
+    d_fw = torch.empty(dpf.xor_fold_workspace_size(), dtype=torch.uint8, device=c.dev)
+    d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=c.dev)
+
+    def tree(ev):
+        if ev:
+            ev[0].record(c.stream)
+        dpf.evalfull_subtree_dev(d_keys, kl, nk, logN, pb, prefix, d_bits, d_work, device=c.local, stream=c.stream)
+        if ev:
+            ev[1].record(c.stream)
+
+    def fold(ev):
+        if ev:
+            ev[0].record(c.stream)
+        dpf.xor_fold_dev(d_bits, per_key, nk, d_db, hi - lo, 32, d_ans, d_fw, device=c.local, stream=c.stream)
+        if ev:
+            ev[1].record(c.stream)
+
+    _, t_ms = c.timed(tree, steps, 3)
+    _, f_ms = c.timed(fold, steps, 3)
+    blocks = nk * (3 * (1 << (stop_of(logN) - pb)) - 2)
+    fold_bytes = (hi - lo) * 32 + nk * per_key          # DB slice + selection bits, read once
+    gbs = fold_bytes / (f_ms * 1e-3) / 1e9
+    return {"tree": {"kernel_ms": round(t_ms, 4), "aes_blocks_per_s": blocks / (t_ms * 1e-3),
+                     "kernels": "k_unpack + k_evalfull"},
+            "fold": {"kernel_ms": round(f_ms, 4), "kernels": "k_fold* + k_xor_parts",
+                     "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                                  "algorithmic_bytes": fold_bytes,
+                                  "note": "DB slice + selection bits read once per batch; the measured streaming-read "
+                                          "ceiling of this chip is ~6.17 TB/s (tools/hbm_read.hip)"}}}
+
+
 def wl_pir(c: Ctx) -> dict:
     a, dpf = c.args, c.dpf
     from dpf import synth
@@ -702,9 +762,15 @@ def wl_pir(c: Ctx) -> dict:
                                       + " (BASELINE configs[4])", "logN": logN, "batch": nk,
                           "parallelism": f"db-shard x{c.world} + all_gather/XOR"},
                   aes_blocks_per_s=aes * c.world / sec)
-    line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_unpack+k_evalfull+k_fold", k_ms,
-                                    (hi - lo) * 32 + nk * ((hi - lo) // 8) * 2, workload="pir",
+    # The dominant kernel is the tree (LDS-bound); the two phases are timed
+    # apart below, and the top-level roofline is the tree's own.
+    kern = pir_breakdown(c, W, d_db, lo, hi, nk, min(a.steps, 20))
+    line["kernels"] = kern
+    line["roofline"] = prg_roofline(aes / (kern["tree"]["kernel_ms"] * 1e-3), "k_unpack+k_evalfull (PIR tree)",
+                                    kern["tree"]["kernel_ms"], nk * ((hi - lo) // 8), workload="pir",
                                     profiled_shape=(W == 1 and nk == 64))
+    line["roofline"]["step_kernel_ms"] = round(k_ms, 4)
+    line["roofline"]["fold"] = kern["fold"]["roofline"]
     if c.world == 1 and not a.no_sweep:
         # B in {1, 16, 64, 256}; the fold reads the DB once per
         # batch up to 256 keys (pir_kernels.hip plan_fold).
@@ -717,6 +783,36 @@ def wl_pir(c: Ctx) -> dict:
                              "db_GBs": round((hi - lo) * 32 / (km * 1e-3) / 1e9, 1)}
         line["batch_sweep"] = sweep
     return line
+
+
+def sub_workloads(c: Ctx) -> dict:
+    """BASELINE configs[2..4] measured in the same process after the
+    headline's timed region, each through its own timed loop (barrier +
+    synchronize, max over ranks): compact forms of the --workload eval /
+    split / pir lines, so the default run (what the driver records) shows all
+    four GPU configs.  Their CPU baselines are added by finalize()."""
+    a = c.args
+    saved = dict(vars(a))
+    a.steps, a.warmup = min(a.steps, 20), min(a.warmup, 5)
+    a.no_api, a.no_sweep, a.emulate_world = True, True, 1
+    out = {}
+    try:
+        for name, fn in (("eval", wl_eval), ("split", wl_split), ("pir", wl_pir)):
+            ln = fn(c)
+            keep = {k: ln[k] for k in ("metric", "value", "unit", "ms_per_step", "scaling", "aes_blocks_per_s")}
+            keep["steps"] = a.steps
+            keep["workload"] = ln["config"]["workload"]
+            keep["roofline"] = {k: ln["roofline"][k] for k in ("bound", "achieved", "peak", "unit", "frac",
+                                                             "kernel", "kernel_ms", "traffic")
+                                if k in ln["roofline"]}
+            if "gate" in ln["roofline"]:
+                keep["roofline"]["gate_frac"] = ln["roofline"]["gate"]["frac"]
+            if "kernels" in ln:
+                keep["kernels"] = ln["kernels"]
+            out[name] = keep
+    finally:
+        vars(a).update(saved)
+    return out
 
 
 def spawn_ranks(n: int) -> int:
@@ -788,6 +884,8 @@ def main() -> None:
     ap.add_argument("--no-sweep", action="store_true", help="pir: skip the B in {1,16,64,256} batch sweep")
     ap.add_argument("--strong", action="store_true",
                     help="evalfull: split a fixed --nkeys over the ranks (strong scaling) instead of --nkeys per rank")
+    ap.add_argument("--no-workloads", action="store_true",
+                    help="evalfull: skip the configs[2..4] sub-lines (workloads) of the default run")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--spinup", type=float, default=0.5,
                     help="seconds of untimed steps before the warmup (GPU clock ramp); 0 disables")
@@ -807,6 +905,8 @@ def main() -> None:
         return
     c = Ctx(args)
     line = {"evalfull": wl_evalfull, "eval": wl_eval, "split": wl_split, "pir": wl_pir}[args.workload](c)
+    if args.workload == "evalfull" and not (args.no_workloads or args.strong or args.emulate_world > 1):
+        line["workloads"] = sub_workloads(c)
     if c.rank == 0:
         finalize(line, args, c.world, c.folded)
         print(json.dumps(line), flush=True)
@@ -831,6 +931,15 @@ def finalize(line: dict, args, world: int, folded: bool) -> None:
                                                      min(args.cpu_seconds, 8.0))
         elif args.workload == "pir":
             line["cpu_baseline"] = cpu_baseline_pir(args.pir_logN, args.batch, min(args.cpu_seconds, 8.0))
+        wls = line.get("workloads", {})
+        sub_s = min(args.cpu_seconds, 4.0)
+        if "eval" in wls:
+            wls["eval"]["cpu_baseline"] = cpu_baseline_eval(args.logN, args.eval_keys, args.eval_points, sub_s)
+        if "split" in wls:
+            wls["split"]["cpu_baseline"] = cpu_baseline(20, sub_s)
+            wls["split"]["cpu_baseline"]["note"] = "points/s of the batched EvalFull port at logN=20"
+        if "pir" in wls:
+            wls["pir"]["cpu_baseline"] = cpu_baseline_pir(args.pir_logN, args.batch, sub_s)
     if folded:
         line["folded_ranks"] = True
         line["scaling"] = None

@@ -336,8 +336,12 @@ DevList devices(int* rc) {
 // i < stop and the final CW at k[len-16 : len] (dpf.go:175-176,186-188,206,
 // 219,231-233): any key of at least 17 + 18*stop bytes evaluates without an
 // index panic, including keys whose final CW overlaps the last record.
-int check_key(size_t klen, uint32_t logN) {
-    if (logN > 63) return fail(DPF_ERR_PARAM, "dpf: logN > 63");
+// EvalFull (full) with logN > 63 cannot allocate its 2^(logN-3)-byte output
+// (dpf.go:251 panics in makeslice): DPF_ERR_PARAM.  Eval validates no logN
+// (dpf.go:171-211): any logN with a long enough key evaluates, its path bits
+// above bit 63 read as 0 (path_bit).
+int check_key(size_t klen, uint32_t logN, bool full = true) {
+    if (full && logN > 63) return fail(DPF_ERR_PARAM, "dpf: logN > 63");
     if (klen < 17 + 18 * (size_t)stop_of(logN)) return fail(DPF_ERR_KEYLEN, "dpf: key shorter than 17+18*(logN-7) bytes");
     return DPF_OK;
 }
@@ -605,6 +609,33 @@ size_t eval_work_bytes(size_t nkeys, size_t ppk, uint32_t logN) {
     return pir_ek_bytes(nkeys, logN) + dpfk::eval_frontier_bytes(nkeys, stop_of(logN), ppk);
 }
 
+// The expanded form's layout depends on (nkeys, stop) (tree_ws), so each
+// expanded workspace is recorded here and dpf_evalfull_expanded_dev refuses
+// one expanded for another shape instead of reading misplaced records.
+std::mutex g_exp_mu;
+// Also records whether the byte-sliced planes were built: the T-table back
+// end expands only its own records, and switching to the byte-sliced one
+// later derives them from those (launch_bs_from_ek) on first use.
+struct Expanded {
+    size_t nkeys;
+    uint32_t stop;
+    bool bs;
+};
+std::unordered_map<const void*, Expanded>& g_expanded = *new std::unordered_map<const void*, Expanded>();
+
+// Every entry point that expands keys into a caller's d_work records what it
+// left there (the same tree_ws layout), so a later dpf_evalfull_expanded_dev
+// never reads planes built from other keys; dpf_eval_batch_dev's workspace
+// has another layout past the records and is dropped.
+void note_expanded(const void* d_work, size_t nkeys, uint32_t stop, bool bs) {
+    std::lock_guard<std::mutex> lk(g_exp_mu);
+    g_expanded[d_work] = {nkeys, stop, bs};
+}
+void forget_expanded(const void* d_work) {
+    std::lock_guard<std::mutex> lk(g_exp_mu);
+    g_expanded.erase(d_work);
+}
+
 }  // namespace
 
 extern "C" {
@@ -722,6 +753,15 @@ std::atomic<int> g_small_mode{[] {
 // the GPU round trip (key H2D, launch, output D2H, sync) -- measured on the
 // GPU box's EPYC (profiles/r03/small_calls).
 constexpr uint32_t kSmallFullMaxLogN = 21;
+// Without VAES the host EvalFull runs 1 block per AESENC instead of 4 (two
+// 128-bit chains per node), ~3x slower at these sizes: at logN = 20 ~92 us
+// against the GPU's 80.7, at 19 ~45 against ~65.  An estimate from the
+// VAES / AES-NI ratio of the host kernels, not a separate measurement.
+constexpr uint32_t kSmallFullMaxLogNNoVaes = 19;
+// DPF_SMALL_HOST's ceiling: two host-side levels of the full width (~2.1x the
+// output) and one core; above it the call goes to the GPU.
+constexpr uint32_t kHostFullMaxLogN = 28;
+uint32_t small_full_max() { return dpfh::host_eval_vaes() ? kSmallFullMaxLogN : kSmallFullMaxLogNNoVaes; }
 
 int dpf_set_small_call_path(int mode) {
     if (mode != DPF_SMALL_AUTO && mode != DPF_SMALL_GPU && mode != DPF_SMALL_HOST)
@@ -729,7 +769,7 @@ int dpf_set_small_call_path(int mode) {
     return g_small_mode.exchange(mode);
 }
 int dpf_get_small_call_path(void) { return g_small_mode.load(); }
-uint32_t dpf_small_call_max_logN(void) { return kSmallFullMaxLogN; }
+uint32_t dpf_small_call_max_logN(void) { return small_full_max(); }
 
 // Route a single call to the host?  Only with a gfx950 device open (so the
 // host path is never a stand-in for a missing GPU) and AES-NI present.
@@ -742,8 +782,8 @@ int route_host(bool full, uint32_t logN) {
         (void)pick_devs(1, &g);
         if (g <= 0) return g;
     }
-    if (mode == DPF_SMALL_HOST) return 1;
-    return !full || logN <= kSmallFullMaxLogN ? 1 : 0;
+    if (mode == DPF_SMALL_HOST) return !full || logN <= kHostFullMaxLogN ? 1 : 0;
+    return !full || logN <= small_full_max() ? 1 : 0;
 }
 
 int dpf_evalfull(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out) {
@@ -751,7 +791,11 @@ int dpf_evalfull(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out) {
     const int h = route_host(true, logN);
     if (h < 0) return h;
     if (h) {
-        dpfh::evalfull_host(key, klen, logN, out);
+        try {
+            dpfh::evalfull_host(key, klen, logN, out);
+        } catch (const std::bad_alloc&) {
+            return fail(DPF_ERR_NOMEM, "dpf: host EvalFull allocation failed");
+        }
         return DPF_OK;
     }
     return dpf_evalfull_batch(key, klen, 1, logN, out, 1);
@@ -759,7 +803,7 @@ int dpf_evalfull(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* out) {
 
 int dpf_eval_batch(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_t* xs, size_t ppk, uint32_t logN,
                    uint8_t* out, int ngpus) {
-    if (int rc = check_key(klen, logN)) return rc;
+    if (int rc = check_key(klen, logN, false)) return rc;
     if (nkeys == 0 || ppk == 0) return DPF_OK;
     int g = 0;
     const DevList devs = pick_devs(ngpus, &g);
@@ -771,7 +815,7 @@ int dpf_eval_batch(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_
 }
 
 int dpf_eval(const uint8_t* key, size_t klen, uint64_t x, uint32_t logN, uint8_t* out_bit) {
-    if (int rc = check_key(klen, logN)) return rc;
+    if (int rc = check_key(klen, logN, false)) return rc;
     const int h = route_host(false, logN);
     if (h < 0) return h;
     if (h) {
@@ -827,7 +871,9 @@ int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t klen, siz
     DeviceGuard g(device);
     const TreeWs w = tree_ws(d_work, nkeys, stop);
     const bool bs = want_bs();
+    forget_expanded(d_work);
     HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, (hipStream_t)stream, bs));
+    note_expanded(d_work, nkeys, stop, bs);
     HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, d_out, (uint64_t)16 << (stop - prefix_bits),
                      (hipStream_t)stream, bs));
     return DPF_OK;
@@ -843,17 +889,18 @@ size_t dpf_eval_workspace_size(size_t nkeys, size_t pts_per_key, uint32_t logN) 
 }
 
 uint32_t dpf_eval_frontier_level(uint32_t logN, size_t pts_per_key) {
-    return dpfk::eval_frontier_level(stop_of(logN), pts_per_key);
+    return logN > 63 ? 0 : dpfk::eval_frontier_level(stop_of(logN), pts_per_key);   // launch_eval: no frontier above 63
 }
 
 int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, const uint64_t* d_xs,
                        size_t ppk, uint32_t logN, uint8_t* d_out, void* d_work, size_t work_bytes, void* stream) {
-    if (int rc = check_key(klen, logN)) return rc;
+    if (int rc = check_key(klen, logN, false)) return rc;
     if (nkeys == 0 || ppk == 0) return DPF_OK;
     const uint32_t stop = stop_of(logN);
     const size_t ekb = pir_ek_bytes(nkeys, logN);
     if (work_bytes < nkeys * dpfk::ek_words(stop) * 4) return fail(DPF_ERR_PARAM, "dpf: Eval workspace too small");
     DeviceGuard g(device);
+    forget_expanded(d_work);
     HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop, (uint32_t*)d_work, (hipStream_t)stream));
     // The frontier (if it fits in the rest of the workspace) lets queries share the tree's top levels.
     void* frontier = work_bytes > ekb ? (uint8_t*)d_work + ekb : nullptr;
@@ -862,29 +909,20 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     return DPF_OK;
 }
 
-// The expanded form's layout depends on (nkeys, stop) (tree_ws), so each
-// expanded workspace is recorded here and dpf_evalfull_expanded_dev refuses
-// one expanded for another shape instead of reading misplaced records.
-std::mutex g_exp_mu;
-// Also records whether the byte-sliced planes were built: the T-table back
-// end expands only its own records, and switching to the byte-sliced one
-// later derives them from those (launch_bs_from_ek) on first use.
-struct Expanded {
-    size_t nkeys;
-    uint32_t stop;
-    bool bs;
-};
-std::unordered_map<const void*, Expanded>& g_expanded = *new std::unordered_map<const void*, Expanded>();
-
 int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN, void* d_work,
                         void* stream) {
     if (int rc = check_key(klen, logN)) return rc;
     DeviceGuard g(device);
     const bool bs = want_bs();
+    forget_expanded(d_work);
     HIP_TRY(expand_keys(d_keys, klen, nkeys, stop_of(logN), tree_ws(d_work, nkeys, stop_of(logN)), (hipStream_t)stream,
                         bs));
-    std::lock_guard<std::mutex> lk(g_exp_mu);
-    g_expanded[d_work] = {nkeys, stop_of(logN), bs};
+    note_expanded(d_work, nkeys, stop_of(logN), bs);
+    return DPF_OK;
+}
+
+int dpf_forget_workspace(const void* d_work) {
+    forget_expanded(d_work);
     return DPF_OK;
 }
 
@@ -902,11 +940,13 @@ int dpf_evalfull_expanded_dev(int device, void* d_work, size_t nkeys, uint32_t l
         if (it == g_expanded.end() || it->second.nkeys != nkeys || it->second.stop != stop)
             return fail(DPF_ERR_PARAM, "dpf: d_work was not expanded by dpf_expand_keys_dev for this nkeys and logN");
         build_bs = bs && !it->second.bs;
-        if (build_bs) it->second.bs = true;
     }
     DeviceGuard g(device);
     const TreeWs w = tree_ws(d_work, nkeys, stop);
-    if (build_bs) HIP_TRY(dpfk::launch_bs_from_ek(w.ek, nkeys, stop, w.ekb, (hipStream_t)stream));
+    if (build_bs) {
+        HIP_TRY(dpfk::launch_bs_from_ek(w.ek, nkeys, stop, w.ekb, (hipStream_t)stream));
+        note_expanded(d_work, nkeys, stop, true);   // only once the planes' launch is enqueued
+    }
     const uint64_t stride = (uint64_t)16 << (stop - prefix_bits);
     HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, d_out, stride, (hipStream_t)stream, bs));
     return DPF_OK;
@@ -941,7 +981,9 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
     const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
     const bool bs = want_bs();
+    forget_expanded(d_work);
     HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st, bs));
+    note_expanded(d_work, nkeys, stop, bs);
     HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st, bs));
     uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
     HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, 32, (uint32_t)nkeys, (uint32_t*)d_ans,

@@ -65,6 +65,9 @@ struct CW {
 };
 
 __device__ __forceinline__ uint32_t tmask(uint32_t t) { return t != 0 ? 0xffffffffu : 0u; }
+// Eval's path bit with Go's shift semantics (dpf.go:194: a shift of 64 or
+// more gives 0, so logN > 63 keys go left on their top logN-64 levels).
+__device__ __forceinline__ uint32_t path_bit(uint64_t x, uint32_t s) { return s < 64 ? (uint32_t)(x >> s) & 1u : 0u; }
 
 // Expanded key record (words): [0..3] root seed, [4] root t, [8+8l..] level l
 // {sCW[4], tLCW, tRCW, 0, 0}, [8+8*stop..+3] final CW.
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval(const uint32_t* __restrict__
     }
     for (uint32_t i = lvl; i < stop; ++i) {
         CW cw = load_cw(ek, i);
-        walk_step<DPF_EVAL_BATCH>(tab, lo, n, cw, (uint32_t)(x >> (logN - 1 - i)) & 1u);
+        walk_step<DPF_EVAL_BATCH>(tab, lo, n, cw, path_bit(x, logN - 1 - i));
     }
     Blk o = mmo1<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n.s);
     o = leaf_fix(o, n.t, load_blk(ek + 8 + 8 * stop));
@@ -547,8 +550,7 @@ __device__ __forceinline__ void eval_pair(const uint32_t* __restrict__ ekeys, ui
     Node n1 = eval_start(ek1, key1, x1, logN, fseed, ft, L);
     for (uint32_t i = fseed != nullptr ? L : 0; i < stop; ++i) {
         const CW cw0 = load_cw(ek0, i), cw1 = load_cw(ek1, i);
-        walk_step2<DPF_EVAL_BATCH>(tab, lo, n0, cw0, (uint32_t)(x0 >> (logN - 1 - i)) & 1u, n1, cw1,
-                                   (uint32_t)(x1 >> (logN - 1 - i)) & 1u);
+        walk_step2<DPF_EVAL_BATCH>(tab, lo, n0, cw0, path_bit(x0, logN - 1 - i), n1, cw1, path_bit(x1, logN - 1 - i));
     }
     Blk o0, o1;
     mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n0.s, o0, KeyFixed<false>{}, n1.s, o1);
@@ -781,7 +783,7 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
     }();
     const uint64_t nkeys = nq / pts_per_key;
     uint32_t L = eval_frontier_level(stop, pts_per_key);
-    if (plain || frontier == nullptr || frontier_bytes < eval_frontier_bytes(nkeys, stop, pts_per_key)) L = 0;
+    if (logN > 63 || plain || frontier == nullptr || frontier_bytes < eval_frontier_bytes(nkeys, stop, pts_per_key)) L = 0;
     const uint4* fseed = nullptr;
     const uint8_t* ft = nullptr;
     if (L > 0) {

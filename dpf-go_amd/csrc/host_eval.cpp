@@ -74,7 +74,7 @@ __attribute__((target("aes,sse4.1"))) void eval_group(const uint8_t* const* keys
         bool right[kQ];
         const __m128i* rk[kQ];          // the path child's key schedule: no per-round select
         for (int q = 0; q < n; ++q) {
-            right[q] = (xs[q] >> (logN - 1 - i)) & 1;               // dpf.go:194-200
+            right[q] = path_bit(xs[q], (uint64_t)logN - 1 - i) != 0;   // dpf.go:194-200
             rk[q] = right[q] ? rr : rl;
             st[q] = _mm_xor_si128(s[q], rk[q][0]);
         }
@@ -255,6 +255,7 @@ __attribute__((target("vaes,avx512f,aes,sse4.1"))) void leaves_vaes(const Level&
 }  // namespace
 
 bool host_eval_available() { return host_has_aesni(); }
+bool host_eval_vaes() { return has_vaes(); }
 
 void eval_batch_host(const uint8_t* keys, size_t klen, size_t nkeys, const uint64_t* xs, size_t ppk, uint32_t logN,
                      uint8_t* out) {

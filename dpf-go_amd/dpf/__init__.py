@@ -79,6 +79,7 @@ SIGNATURES = {
     "dpf_eval_batch_dev": (_int, [_int, _vp, _sz, _sz, _vp, _sz, _u32, _vp, _vp, _sz, _vp]),
     "dpf_expand_keys_dev": (_int, [_int, _vp, _sz, _sz, _u32, _vp, _vp]),
     "dpf_evalfull_expanded_dev": (_int, [_int, _vp, _sz, _u32, _u32, _u64, _vp, _vp]),
+    "dpf_forget_workspace": (_int, [_vp]),
     "dpf_set_small_call_path": (_int, [_int]),
     "dpf_get_small_call_path": (_int, []),
     "dpf_small_call_max_logN": (ctypes.c_uint32, []),
@@ -166,6 +167,11 @@ def gpu_init_devices(ordinals: Sequence[int]) -> int:
 
 def gpu_shutdown() -> None:
     lib().dpf_gpu_shutdown()
+
+
+def gpu_count() -> int:
+    """Devices the library has open (dpf_gpu_count)."""
+    return int(lib().dpf_gpu_count())
 
 
 # ------------------------------------------------------- key wire format ---
@@ -351,6 +357,11 @@ def evalfull_expanded_dev(d_work, nkeys: int, logN: int, d_out, prefix_bits: int
                           device: int = 0, stream=None) -> None:
     _check(lib().dpf_evalfull_expanded_dev(device, _ptr(d_work), nkeys, logN, prefix_bits, prefix, _ptr(d_out),
                                            _stream_handle(stream)))
+
+
+def forget_workspace(d_work) -> None:
+    """Drop the library's record of what was expanded into d_work (call before freeing it)."""
+    _check(lib().dpf_forget_workspace(_ptr(d_work)))
 
 
 def set_aes_impl(impl) -> int:

@@ -196,3 +196,14 @@ func SetSmallCallPath(mode int) int {
 	}
 	return int(rc)
 }
+
+// GetSmallCallPath returns the current small-call route (dpf_get_small_call_path).
+func GetSmallCallPath() int {
+	return int(C.dpf_get_small_call_path())
+}
+
+// SmallCallMaxLogN is the largest logN whose single-key EvalFull SmallAuto
+// routes to the host (dpf_small_call_max_logN).
+func SmallCallMaxLogN() uint64 {
+	return uint64(C.dpf_small_call_max_logN())
+}

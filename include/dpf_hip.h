@@ -92,7 +92,12 @@ int dpf_keys_unpack(const uint8_t* packed, size_t key_len, size_t n, uint8_t* co
 /* Keys: at least 17 + 18*stop bytes (the reference's own index bound,
  * dpf.go:175-176,186-188); the final CW is always k[len-16 : len]
  * (dpf.go:206,219), longer keys are accepted.  Shorter: DPF_ERR_KEYLEN. */
-/* Eval (dpf.go:171-211): *out_bit = 0/1. */
+/* Eval (dpf.go:171-211): *out_bit = 0/1.  Like the reference, Eval accepts
+ * any logN (Gen never makes a key above 63): path bits above bit 63 of x read
+ * as 0 (Go's `uint64(1) << s` is 0 for s >= 64, dpf.go:194), so such a key
+ * takes the left child on its top logN-64 levels.  The EvalFull entry points
+ * return DPF_ERR_PARAM for logN > 63, where the reference panics allocating
+ * its 2^(logN-3)-byte output (dpf.go:251). */
 int dpf_eval(const uint8_t* key, size_t key_len, uint64_t x, uint32_t logN, uint8_t* out_bit);
 /* Host output buffers are written by parallel copies from pinned staging;
  * with DPF_PREFAULT_OUTPUT=1 in the environment, buffers >= 64 MiB also get
@@ -180,6 +185,12 @@ int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t key_len, size_
                         void* stream);
 int dpf_evalfull_expanded_dev(int device, void* d_work, size_t nkeys, uint32_t logN, uint32_t prefix_bits,
                               uint64_t prefix, uint8_t* d_out, void* stream);
+/* The library remembers, per d_work address, what dpf_expand_keys_dev (and
+ * the other _dev entry points that expand into a caller's workspace) left
+ * there.  Call this before freeing a workspace: a new buffer later allocated
+ * at the same address would otherwise pass dpf_evalfull_expanded_dev's
+ * shape check with stale records.  Always returns 0. */
+int dpf_forget_workspace(const void* d_work);
 
 /* ---- 2-server PIR over a DPF (BASELINE configs[4]; no reference
  *      counterpart: a consumer of EvalFull, SURVEY 8a last row) -----------

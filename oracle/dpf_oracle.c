@@ -274,7 +274,9 @@ static uint8_t eval_with(mmo_fn f, const uint8_t* k, size_t klen, uint64_t x, ui
             tL ^= k[17 + i * 18 + 16];
             tR ^= k[17 + i * 18 + 17];
         }
-        if (x & ((uint64_t)1 << (logN - 1 - i))) { memcpy(s, sR, 16); t = tR; }
+        /* :194 -- Go's `uint64(1) << n` is 0 for n >= 64 (C leaves it undefined) */
+        uint64_t sh = logN - 1 - i, m = sh < 64 ? (uint64_t)1 << sh : 0;
+        if (x & m)                                { memcpy(s, sR, 16); t = tR; }
         else                                      { memcpy(s, sL, 16); t = tL; }
     }
     f(RK_L, s, s);                                                 /* :204 */

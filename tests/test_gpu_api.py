@@ -81,3 +81,39 @@ def test_expanded_form_builds_byte_sliced_records_on_first_use():
             assert np.array_equal(d_out.cpu().numpy().reshape(nk, olen), want)
     finally:
         dpf.set_aes_impl(prev)
+
+
+def test_workspace_reexpanded_by_another_entry_point_is_not_stale():
+    """a workspace registered with byte-sliced planes, then
+    re-expanded with OTHER keys by dpf_evalfull_subtree_dev under the T-table
+    back end, must not be evaluated from the old planes when the caller
+    switches back to byte-sliced: the registry follows every expansion.
+    dpf_forget_workspace drops the record (the next expanded call refuses)."""
+    import torch
+    logN, nk = 16, 8
+    kl, olen = dpf.key_len(logN), dpf.evalfull_len(logN)
+    al, s0, s1 = synth.key_seeds(nk, logN, first=404)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    al2, s02, s12 = synth.key_seeds(nk, logN, first=505)
+    kb, _ = dpf.gen_batch_seeded(al2, logN, s02, s12)
+    d_a = torch.from_numpy(ka.reshape(-1)).cuda()
+    d_b = torch.from_numpy(kb.reshape(-1)).cuda()
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device="cuda")
+    d_out = torch.zeros(nk * olen, dtype=torch.uint8, device="cuda")
+    prev = dpf.set_aes_impl("bitsliced")
+    try:
+        dpf.expand_keys_dev(d_a, kl, nk, logN, d_work)           # planes of keys A
+        dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)
+        dpf.set_aes_impl("ttable")
+        dpf.evalfull_subtree_dev(d_b, kl, nk, logN, 0, 0, d_out, d_work)   # records of keys B only
+        dpf.set_aes_impl("bitsliced")
+        d_out.zero_()
+        dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)        # must rebuild planes from B
+        torch.cuda.synchronize()
+        assert np.array_equal(d_out.cpu().numpy().reshape(nk, olen), oracle.evalfull_batch(kb, logN, nthreads=4))
+        dpf.forget_workspace(d_work)
+        with pytest.raises(dpf.DPFPanic) as e:
+            dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)
+        assert e.value.code == dpf.DPF_ERR_PARAM
+    finally:
+        dpf.set_aes_impl(prev)

@@ -7,7 +7,7 @@ OUT="$REPO/$1"; WL="$2"; shift 2
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-BENCH=(python3 "$REPO/bench.py" --workload "$WL" --steps 5 --warmup 2 --no-cpu-baseline --no-sweep --no-api --no-variants "$@")
+BENCH=(python3 "$REPO/bench.py" --workload "$WL" --steps 5 --warmup 2 --no-cpu-baseline --no-sweep --no-api --no-variants --no-workloads "$@")
 i=0
 for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
