@@ -991,6 +991,62 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     return DPF_OK;
 }
 
+size_t dpf_pir_db_sliced_size(uint64_t nrec) { return std::max<size_t>(16, dpfk::pir_sliced_bytes(nrec)); }
+
+int dpf_pir_db_slice_dev(int device, const uint8_t* d_db, uint64_t nrec, uint8_t* d_dbs, void* stream) {
+    if (nrec > 0 && (!d_db || !d_dbs)) return fail(DPF_ERR_PARAM, "dpf: null device buffer");
+    if (((uintptr_t)d_db | (uintptr_t)d_dbs) % 16 != 0) return fail(DPF_ERR_PARAM, "dpf: misaligned device buffer");
+    DeviceGuard g(device);
+    HIP_TRY(dpfk::launch_slice_db(d_db, nrec, d_dbs, (hipStream_t)stream));
+    return DPF_OK;
+}
+
+int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t klen, size_t nkeys, uint32_t logN,
+                              uint32_t prefix_bits, uint64_t prefix, const uint8_t* d_dbs, uint64_t nrec,
+                              uint8_t* d_ans, void* d_work, void* stream) {
+    if (int rc = check_key(klen, logN)) return rc;
+    const uint32_t stop = stop_of(logN);
+    if (prefix_bits > stop || (prefix >> prefix_bits) != 0) return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
+    const uint64_t slice = logN - prefix_bits >= 64 ? ~0ull : (1ull << (logN - prefix_bits));
+    if (nrec > slice) return fail(DPF_ERR_PARAM, "dpf: more DB records than the subtree's domain");
+    if ((uintptr_t)d_dbs % 16 != 0) return fail(DPF_ERR_PARAM, "dpf: misaligned device buffer");
+    DeviceGuard g(device);
+    hipStream_t st = (hipStream_t)stream;
+    if (nkeys == 0) return DPF_OK;
+    if (nrec == 0) {
+        HIP_TRY(hipMemsetAsync(d_ans, 0, nkeys * 32, st));
+        return DPF_OK;
+    }
+    // The same workspace and tree pass as dpf_pir_answer_dev; the fold reads the sliced DB.
+    const TreeWs w = tree_ws(d_work, nkeys, stop);
+    uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
+    const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
+    const bool bs = want_bs();
+    forget_expanded(d_work);
+    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st, bs));
+    note_expanded(d_work, nkeys, stop, bs);
+    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st, bs));
+    uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
+    HIP_TRY(dpfk::launch_pir_fold_sliced((const uint32_t*)bits, per_key / 4, d_dbs, nrec, (uint32_t)nkeys,
+                                         (uint32_t*)d_ans, parts, st));
+    return DPF_OK;
+}
+
+int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_dbs,
+                            uint64_t nrec, uint8_t* d_ans, void* d_work, void* stream) {
+    if (bits_stride % 16 != 0) return fail(DPF_ERR_PARAM, "dpf: bits_stride must be a multiple of 16");
+    if (nrec > (uint64_t)bits_stride * 8) return fail(DPF_ERR_PARAM, "dpf: more records than selection bits per key");
+    if (((uintptr_t)d_bits | (uintptr_t)d_dbs) % 16 != 0 || (uintptr_t)d_ans % 4 != 0)
+        return fail(DPF_ERR_PARAM, "dpf: misaligned device buffer");
+    if (nkeys > 0 && (!d_ans || !d_work || (nrec > 0 && (!d_bits || !d_dbs))))
+        return fail(DPF_ERR_PARAM, "dpf: null device buffer");
+    DeviceGuard g(device);
+    if (nkeys == 0) return DPF_OK;
+    HIP_TRY(dpfk::launch_pir_fold_sliced((const uint32_t*)d_bits, bits_stride / 4, d_dbs, nrec, (uint32_t)nkeys,
+                                         (uint32_t*)d_ans, (uint32_t*)d_work, (hipStream_t)stream));
+    return DPF_OK;
+}
+
 size_t dpf_xor_fold_workspace_size(void) { return dpfk::pir_fold_parts_bytes(); }
 
 int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_payload,

@@ -7,7 +7,7 @@ namespace dpfh {
 
 inline uint32_t stop_of(uint32_t logN) { return logN >= 7 ? logN - 7 : 0; }
 inline size_t key_len(uint32_t logN) { return 33 + 18 * (size_t)stop_of(logN); }
-inline size_t full_len(uint32_t logN) { return logN >= 7 ? ((size_t)1 << (logN - 3)) : 16; }
+inline size_t full_len(uint32_t logN) { return logN > 63 ? 0 : logN >= 7 ? ((size_t)1 << (logN - 3)) : 16; }   // 0: no such output
 // Bit `s` of x with Go's shift semantics: Eval's path test
 // `x & (uint64(1) << (logN-1-i))` (dpf.go:194) is 0 once the shift reaches
 // 64, so a logN > 63 key takes the left child on its top logN-64 levels.

@@ -617,6 +617,279 @@ hipError_t fold_pass(const FoldArgs& a, bool direct, int kw, uint32_t* ans, uint
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// The fold as a GF(2) matrix product on the matrix cores.
+//
+//   count[k][n] = sum_i sel[k][i] * dbbit[i][n],   ans bit (k, n) = count & 1
+//
+// is a {0,1} product of [keys x records] by [records x 256 bit positions], so
+// it runs on v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 (FP4) operands: every
+// product is exactly 1 or 0, the fp32 accumulators hold exact counts (far
+// below 2^24 per wave), and the parity is the answer bit.  No LDS at all.
+//
+// Operands.  An MFMA operand lane holds 32 K-values (records) of ONE row
+// (key) or column (bit position); the K order inside the lane is ours to
+// pick as long as A and B agree.  The key side is EvalFull's own layout: one
+// selection word = 32 consecutive records of one key.  The DB side needs the
+// transposed form -- for bit position n, one word of 32 consecutive records
+// -- which the PIR server builds once when the DB is loaded (the "sliced"
+// layout, k_slice_db below):
+//   dbs[S][n][g] (u32), S = super-group of 256 records, n < 256 bit position,
+//   g < 8 record group; bit j = bit n of record 256 S + 32 g + j.
+// A lane (n, h) loads dbs[S][n][4h .. 4h+3] and a key lane (k, h) loads
+// selection words 8S + 4h .. +3 (one dwordx4 each, both coalesced): K-block
+// t < 4 of super-group S is record groups t (h = 0) and 4 + t (h = 1).
+// Word -> FP4 operand in registers, nibble i of dword d = record 4i + d:
+//   DB    d0 = x & 0x1..  (0.5)  d1 = x & 0x2.. (1.0)  d2 = x & 0x4.. (2.0)
+//         d3 = (x >> 1) & 0x4.. (2.0)                       5 VALU per word
+//   keys  d0 = (s << 2) & 0x4.. (2.0)  d1 = s & 0x2.. (1.0)
+//         d2 = (s >> 2) & 0x1.. (0.5)  d3 = (s >> 3) & 0x1.. (0.5)
+// so every nonzero product is exactly 1 with unit (E8M0 127) scales.
+//
+// Mapping.  A wave covers MT key tiles (32 keys) x NT bit tiles (32 bit
+// positions) of a contiguous run of super-groups; the 8/NT waves of a
+// workgroup split the record's 256 bits and share its selection words (L1).
+// At the end each accumulator register's parities become two answer words by
+// one ballot (C/D layout: lane = column n, register e = rows (e&3) +
+// 8(e>>2) + 4h), written to the workgroup's partial; k_xor_parts combines.
+typedef int fold_v8i __attribute__((ext_vector_type(8)));
+typedef float fold_v16f __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ fold_v8i fp4_db(uint32_t x) {
+    fold_v8i r;
+    r[0] = (int)(x & 0x11111111u);
+    r[1] = (int)(x & 0x22222222u);
+    r[2] = (int)(x & 0x44444444u);
+    r[3] = (int)((x >> 1) & 0x44444444u);
+    r[4] = r[5] = r[6] = r[7] = 0;
+    return r;
+}
+__device__ __forceinline__ fold_v8i fp4_sel(uint32_t s) {
+    fold_v8i r;
+    r[0] = (int)((s << 2) & 0x44444444u);
+    r[1] = (int)(s & 0x22222222u);
+    r[2] = (int)((s >> 2) & 0x11111111u);
+    r[3] = (int)((s >> 3) & 0x11111111u);
+    r[4] = r[5] = r[6] = r[7] = 0;
+    return r;
+}
+__device__ __forceinline__ uint32_t u4w(const uint4& v, int t) { return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w; }
+
+constexpr int kFoldFp4 = 4;         // cbsz / blgp format code of e2m1
+constexpr int kE8M0One = 127;       // block scale 2^0
+
+// Selection words reach the waves through LDS: per block of kSelSG
+// super-groups the workgroup copies each key's 128-byte span (one whole line
+// per key, coalesced) into a padded row, and the next block's lines are in
+// flight in registers while this one is folded.  (Loaded straight into the
+// operand lanes, 16 B per lane from 32 rows 2 MiB apart, the fold fetched
+// ~1.6x its bytes and ran at a third of the HBM rate: profiles/r04/fold_v1.)
+constexpr int kSelSG = 4;                       // super-groups per staged block: 128 B per key
+constexpr int kSelRow = kSelSG * 8 + 4;         // words per staged row (+4: conflict-free ds_read_b128)
+
+template <int MT, int NT>
+__global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
+    const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
+    uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words) {
+    constexpr int NW = 8 / NT;
+    constexpr int kRows = 32 * MT;
+    constexpr int kPieces = kRows * (kSelSG * 8 / 4);          // uint4 pieces per staged block
+    constexpr int kPer = (kPieces + 64 * NW - 1) / (64 * NW);  // per thread
+    __shared__ __attribute__((aligned(16))) uint32_t s_sel[kRows * kSelRow];
+    zero_answers(zero, zero_words);
+    const uint32_t l = threadIdx.x & 63, h = l >> 5, r = l & 31;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t s0 = (uint64_t)blockIdx.x * sg_per_block;
+    const uint64_t s1 = s0 + sg_per_block < nsg ? s0 + sg_per_block : nsg;
+    if (s0 >= s1) return;                                       // uniform over the workgroup
+    // Staging role: piece p = threadIdx.x + i*64*NW is row p/8, 16 bytes p%8.
+    auto load_sel = [&](uint64_t sb, uint4 (&v)[kPer]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const uint32_t p = threadIdx.x + (uint32_t)i * 64 * NW;
+            const uint32_t row = p >> 3, q = p & 7;
+            const uint64_t word = sb * 8 + 4 * q;
+            const bool ok = p < (uint32_t)kPieces && row < nkeys && word + 4 <= wpk;
+            const uint4 x = *reinterpret_cast<const uint4*>(bits + (uint64_t)(ok ? row : 0) * wpk + (ok ? word : 0));
+            v[i] = ok ? x : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_sel = [&](const uint4 (&v)[kPer]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const uint32_t p = threadIdx.x + (uint32_t)i * 64 * NW;
+            if (p < (uint32_t)kPieces)
+                *reinterpret_cast<uint4*>(&s_sel[(p >> 3) * kSelRow + 4 * (p & 7)]) = v[i];
+        }
+    };
+    auto load_db = [&](uint64_t S, uint4 (&B)[NT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) B[j] = dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h];
+    };
+    fold_v16f acc[MT][NT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[m][j][e] = 0.0f;
+    uint4 sv[kPer];
+    load_sel(s0, sv);
+    uint4 B0[NT], B1[NT];
+    load_db(s0, B0);
+    // One super-group: 4 K-blocks of 64 records x MT x NT MFMAs.
+    auto fold_sg = [&](uint32_t sl, const uint4 (&B)[NT]) __attribute__((always_inline)) {
+        uint4 A[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+            A[m] = *reinterpret_cast<const uint4*>(&s_sel[(32 * m + r) * kSelRow + 8 * sl + 4 * h]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            fold_v8i bo[NT];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bo[j] = fp4_db(u4w(B[j], t));
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const fold_v8i ao = fp4_sel(u4w(A[m], t));
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ao, bo[j], acc[m][j], kFoldFp4, kFoldFp4,
+                                                                               0, kE8M0One, 0, kE8M0One);
+            }
+        }
+    };
+    for (uint64_t sb = s0; sb < s1; sb += kSelSG) {
+        fold_prio(sb - s0, s1 - s0);
+        __syncthreads();                                        // previous block's operand reads are done
+        store_sel(sv);
+        __syncthreads();
+        const uint64_t nb = sb + kSelSG < s1 ? sb + kSelSG : sb;   // next block in flight (clamped)
+        load_sel(nb, sv);
+        const uint32_t n = s1 - sb < (uint64_t)kSelSG ? (uint32_t)(s1 - sb) : (uint32_t)kSelSG;
+        // Super-groups of the block in pairs: the DB pieces ping-pong, the
+        // next one in flight while this one folds.
+        for (uint32_t sl = 0; sl < n; sl += 2) {
+            const uint64_t S = sb + sl;
+            load_db(S + 1 < s1 ? S + 1 : S, B1);
+            fold_sg(sl, B0);
+            if (sl + 1 < n) {
+                load_db(S + 2 < s1 ? S + 2 : S + 1, B0);
+                fold_sg(sl + 1, B1);
+            } else {
+#pragma unroll
+                for (int j = 0; j < NT; ++j) B0[j] = B1[j];
+            }
+        }
+    }
+    // Parities -> answer words: parts[block][key][8] (word = bit tile).
+    constexpr uint32_t pkeys = 32 * MT;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            uint32_t out = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const uint32_t p = ((uint32_t)acc[m][j][e]) & 1u;
+                const uint64_t b = __builtin_amdgcn_ballot_w64(p != 0);
+                const uint32_t row0 = (e & 3) + 8 * (e >> 2);
+                out = l == row0 ? (uint32_t)b : out;
+                out = l == row0 + 4 ? (uint32_t)(b >> 32) : out;
+            }
+            if (l < 32) parts[((uint64_t)blockIdx.x * pkeys + 32 * m + l) * 8 + w * NT + j] = out;
+        }
+}
+
+// The sliced layout (above) from a row-major DB of 32-byte records: one wave
+// per 64 records (record groups 2q', 2q'+1 of a super-group); lane l holds
+// record l's 8 words and one ballot per bit position transposes 32 x 32 bits.
+__global__ __launch_bounds__(256) void k_slice_db(const uint4* __restrict__ db, uint64_t nrec,
+                                                   uint32_t* __restrict__ dbs, uint64_t nwaves) {
+    const uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (q >= nwaves) return;
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t rec = q * 64 + l;
+    uint4 a = make_uint4(0, 0, 0, 0), b = a;
+    if (rec < nrec) {
+        a = db[2 * rec];
+        b = db[2 * rec + 1];
+    }
+    const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint64_t S = q >> 2;
+    const uint32_t g = 2 * (uint32_t)(q & 3) + (l >> 5);
+#pragma unroll
+    for (int wi = 0; wi < 8; ++wi) {
+        uint32_t out = 0;
+#pragma unroll
+        for (int bb = 0; bb < 32; ++bb) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(((wd[wi] >> bb) & 1u) != 0);
+            out = l == (uint32_t)bb ? (uint32_t)m : out;
+            out = l == (uint32_t)bb + 32 ? (uint32_t)(m >> 32) : out;
+        }
+        dbs[(S * 256 + 32 * wi + (l & 31)) * 8 + g] = out;
+    }
+}
+
+uint64_t pir_sliced_bytes(uint64_t nrec) { return (nrec + 255) / 256 * 256 * 32; }
+
+hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipStream_t st) {
+    const uint64_t nsg = (nrec + 255) / 256;
+    if (nsg == 0) return hipSuccess;
+    const uint64_t nwaves = nsg * 4;
+    hipLaunchKernelGGL(k_slice_db, dim3((uint32_t)((nwaves + 3) / 4)), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(db), nrec, reinterpret_cast<uint32_t*>(dbs), nwaves);
+    return hipGetLastError();
+}
+
+namespace {
+template <int MT, int NT>
+hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
+                          uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st) {
+    constexpr int NW = 8 / NT;
+    // Resident workgroups only (one round): each takes a contiguous run of
+    // whole staged blocks.  (A fixed 4 workgroups per CU left 1/4 - 3/4 of
+    // them for a second round at 3 or 1 resident per CU.)
+    static int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_mfma<MT, NT>, 64 * NW, 0) != hipSuccess || n < 1)
+            n = 1;
+        return n;
+    }();
+    uint64_t spb;
+    split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, kSelSG, blocks, spb);
+    hipLaunchKernelGGL((k_fold_mfma<MT, NT>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+                       reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
+                                  uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
+    if (nkeys == 0) return hipSuccess;
+    if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * 32, st);
+    if (words_per_key % 4 != 0 || words_per_key * 32 < nrec) return hipErrorInvalidValue;
+    const uint64_t nsg = (nrec + 255) / 256;
+    for (uint32_t k0 = 0; k0 < nkeys; k0 += 256) {
+        const uint32_t nk = nkeys - k0 < 256 ? nkeys - k0 : 256;
+        const uint32_t* b = bits + (uint64_t)k0 * words_per_key;
+        uint32_t* zero = k0 == 0 ? ans : nullptr;
+        const uint64_t zw = k0 == 0 ? (uint64_t)nkeys * 8 : 0;
+        uint64_t blocks = 0;
+        uint32_t mt;
+        hipError_t e;
+        if (nk <= 32) e = launch_mfma_mt<1, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 1;
+        else if (nk <= 64) e = launch_mfma_mt<2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 2;
+        else if (nk <= 128) e = launch_mfma_mt<4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 4;
+        else e = launch_mfma_mt<8, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 8;
+        if (e != hipSuccess) return e;
+        const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
+        hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk, 32 * mt,
+                           8u, ans + (uint64_t)k0 * 8, (uint64_t)8, 0u);
+        if (hipError_t e2 = hipGetLastError(); e2 != hipSuccess) return e2;
+    }
+    return hipSuccess;
+}
+
 FoldPlan plan_fold(uint64_t rec_bytes, uint32_t nkeys) {
     FoldPlan p{};
     const uint64_t c = rec_bytes / 32;

@@ -28,4 +28,13 @@ uint64_t pir_fold_parts_bytes();
 hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const uint8_t* db, uint64_t nrec,
                            uint64_t rec_bytes, uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st);
 
+// The MFMA fold (k_fold_mfma, 32-byte records): the same answers from the DB
+// in its bit-sliced layout (dbs, pir_sliced_bytes(nrec) bytes, built once by
+// launch_slice_db from the row-major DB).  Same bits / parts / ans contract
+// as launch_pir_fold.
+uint64_t pir_sliced_bytes(uint64_t nrec);
+hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipStream_t st);
+hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
+                                  uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st);
+
 }  // namespace dpfk

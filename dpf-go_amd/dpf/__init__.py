@@ -90,6 +90,10 @@ SIGNATURES = {
     "dpf_xor_fold_dev": (_int, [_int, _vp, _sz, _sz, _vp, _u64, _sz, _vp, _vp, _vp]),
     "dpf_pir_workspace_size": (_sz, [_sz, _u32, _u32]),
     "dpf_pir_answer_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _u64, _vp, _vp, _vp]),
+    "dpf_pir_db_sliced_size": (_sz, [_u64]),
+    "dpf_pir_db_slice_dev": (_int, [_int, _vp, _u64, _vp, _vp]),
+    "dpf_pir_answer_sliced_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _u64, _vp, _vp, _vp]),
+    "dpf_xor_fold_sliced_dev": (_int, [_int, _vp, _sz, _sz, _vp, _u64, _vp, _vp, _vp]),
     "dpf_pir_db_create": (_int, [_u8p, _u64, _u32, _int, ctypes.POINTER(_vp)]),
     "dpf_pir_answer": (_int, [_vp, _u8p, _sz, _sz, _u8p]),
     "dpf_pir_db_free": (None, [_vp]),
@@ -267,6 +271,8 @@ def _eval_fn():
 
 def EvalFull(key: bytes, logN: int) -> bytes:
     """dpf.go:243 — the share of f_alpha over the whole domain, packed bits."""
+    if logN > 63:   # the reference panics allocating 2^(logN-3) bytes (dpf.go:251)
+        raise DPFPanic(DPF_ERR_PARAM, "dpf: logN > 63")
     kk = _as_u8(key)
     out = np.zeros(evalfull_len(logN), np.uint8)
     _check(lib().dpf_evalfull(_buf(kk), kk.size, logN, _buf(out)))
@@ -430,6 +436,29 @@ def pir_answer_dev(d_keys, key_len_: int, nkeys: int, logN: int, d_db, nrec: int
     """Server answers (nkeys x 32 B) for the DB slice of subtree (prefix_bits, prefix)."""
     _check(lib().dpf_pir_answer_dev(device, _ptr(d_keys), key_len_, nkeys, logN, prefix_bits, prefix, _ptr(d_db),
                                     nrec, _ptr(d_ans), _ptr(d_work), _stream_handle(stream)))
+
+
+def pir_db_sliced_size(nrec: int) -> int:
+    return int(lib().dpf_pir_db_sliced_size(nrec))
+
+
+def pir_db_slice_dev(d_db, nrec: int, d_dbs, device: int = 0, stream=None) -> None:
+    """Bit-sliced copy of a row-major 32-B-record DB for the MFMA fold (built once per DB)."""
+    _check(lib().dpf_pir_db_slice_dev(device, _ptr(d_db), nrec, _ptr(d_dbs), _stream_handle(stream)))
+
+
+def pir_answer_sliced_dev(d_keys, key_len_: int, nkeys: int, logN: int, d_dbs, nrec: int, d_ans, d_work,
+                          prefix_bits: int = 0, prefix: int = 0, device: int = 0, stream=None) -> None:
+    """pir_answer_dev over the bit-sliced DB (the matrix-core fold)."""
+    _check(lib().dpf_pir_answer_sliced_dev(device, _ptr(d_keys), key_len_, nkeys, logN, prefix_bits, prefix,
+                                           _ptr(d_dbs), nrec, _ptr(d_ans), _ptr(d_work), _stream_handle(stream)))
+
+
+def xor_fold_sliced_dev(d_bits, bits_stride: int, nkeys: int, d_dbs, nrec: int, d_ans, d_work, device: int = 0,
+                        stream=None) -> None:
+    """xor_fold_dev for 32-B records over the bit-sliced DB (the matrix-core fold)."""
+    _check(lib().dpf_xor_fold_sliced_dev(device, _ptr(d_bits), bits_stride, nkeys, _ptr(d_dbs), nrec, _ptr(d_ans),
+                                         _ptr(d_work), _stream_handle(stream)))
 
 
 class PirDB:

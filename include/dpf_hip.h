@@ -43,7 +43,7 @@ const char* dpf_last_error(void);
 /* ---- sizes ------------------------------------------------------------ */
 /* len(DPFkey) produced by Gen for this logN (dpf.go:89-167). */
 size_t dpf_key_len(uint32_t logN);
-/* len(EvalFull(k, logN)) (dpf.go:248-251). */
+/* len(EvalFull(k, logN)) (dpf.go:248-251); 0 for logN > 63 (no such output). */
 size_t dpf_evalfull_len(uint32_t logN);
 /* Device scratch bytes the _dev entry points need for nkeys keys. */
 size_t dpf_workspace_size(size_t nkeys, uint32_t logN);
@@ -220,6 +220,23 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t key_len, size_t
 size_t dpf_xor_fold_workspace_size(void);
 int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_payload,
                      uint64_t nrec, size_t rec_bytes, uint8_t* d_ans, void* d_work, void* stream);
+
+/* The fold on the matrix cores (v_mfma_scale_f32_32x32x64_f8f6f4, FP4 {0,1}
+ * operands, exact counts whose parity is the answer bit) reads the DB in a
+ * bit-sliced layout that a PIR server builds once when it loads the DB:
+ * dbs[S][n][g] (u32) for super-group S of 256 records, bit position n < 256
+ * and record group g < 8, bit j = bit n of record 256*S + 32*g + j (records
+ * past nrec read as 0).  dpf_pir_db_slice_dev writes it from the row-major
+ * DB (nrec x 32 B) into dpf_pir_db_sliced_size(nrec) bytes.  The _sliced
+ * entry points take that layout and give the same answers as their row-major
+ * forms (same workspace sizes); 32-byte records only. */
+size_t dpf_pir_db_sliced_size(uint64_t nrec);
+int dpf_pir_db_slice_dev(int device, const uint8_t* d_db, uint64_t nrec, uint8_t* d_dbs, void* stream);
+int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t key_len, size_t nkeys, uint32_t logN,
+                              uint32_t prefix_bits, uint64_t prefix, const uint8_t* d_dbs, uint64_t nrec,
+                              uint8_t* d_ans, void* d_work, void* stream);
+int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_dbs,
+                            uint64_t nrec, uint8_t* d_ans, void* d_work, void* stream);
 
 /* Host form: the DB is uploaded once, sharded by top-level subtree over
  * ngpus devices (a power of two), each GPU folds its slice and the host

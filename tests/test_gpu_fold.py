@@ -132,3 +132,63 @@ def test_xor_fold_rejects_bad_shapes():
             dpf.xor_fold_dev(d, stride, 1, d, nrec, rec, d, w)
         assert e.value.code == dpf.DPF_ERR_PARAM
     dpf.xor_fold_dev(d, 16, 0, d, 128, 32, d, w)   # no keys: nothing to do
+
+
+# ---- the matrix-core fold over the bit-sliced DB (dpf_xor_fold_sliced_dev,
+# dpf_pir_answer_sliced_dev): every key tile count (1/2/4/8 x 32 keys), more
+# than one 256-key pass, ragged record counts (the sliced layout pads the last
+# 256-record super-group with zero bits), selection strides that are not a
+# multiple of 8 words, and nrec = 0.
+@pytest.mark.parametrize("logN,nk,nrec", [
+    (7, 1, 128), (9, 3, 300), (12, 33, 4096), (12, 64, 4000), (13, 65, 8192), (13, 128, 8000),
+    (12, 129, 4096), (12, 256, 4096), (12, 300, 3001), (8, 5, 1), (10, 7, 0), (16, 64, 65536 - 77),
+])
+def test_sliced_mfma_fold_matches_oracle(logN, nk, nrec):
+    import torch
+    dev = torch.device("cuda", 0)
+    _, ka, _ = _keys(nk, logN, first=700 + nk)
+    full = dpf.evalfull_batch(ka, logN, ngpus=1)
+    stride = full.shape[1]
+    payload = synth.db_bytes(max(nrec, 1) * 32).reshape(-1, 32)[:nrec]
+    d_full = torch.from_numpy(full.reshape(-1)).to(dev)
+    d_db = torch.from_numpy(np.ascontiguousarray(payload).reshape(-1)).to(dev) if nrec else \
+        torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_dbs = torch.empty(dpf.pir_db_sliced_size(nrec), dtype=torch.uint8, device=dev)
+    dpf.pir_db_slice_dev(d_db, nrec, d_dbs)
+    d_ans = torch.full((nk * 32,), 0xAB, dtype=torch.uint8, device=dev)
+    d_work = torch.empty(dpf.xor_fold_workspace_size(), dtype=torch.uint8, device=dev)
+    dpf.xor_fold_sliced_dev(d_full, stride, nk, d_dbs, nrec, d_ans, d_work)
+    torch.cuda.synchronize()
+    got = d_ans.cpu().numpy().reshape(nk, 32)
+    assert np.array_equal(got, _want(full, payload.reshape(-1, 32), nrec))
+    if nrec:
+        assert np.array_equal(got, _fold(d_full, stride, nk, payload, nrec, 32))
+
+
+def test_sliced_pir_answer_two_server_full_size():
+    """configs[4] through the MFMA fold: logN=24, 2^24 x 32 B, B=64 and 256:
+    answers equal the LDS fold's and the two servers XOR to DB[alpha]."""
+    import torch
+    dev = torch.device("cuda", 0)
+    logN = 24
+    nrec = 1 << logN
+    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    d_db = torch.from_numpy(db.reshape(-1)).to(dev)
+    d_dbs = torch.empty(dpf.pir_db_sliced_size(nrec), dtype=torch.uint8, device=dev)
+    dpf.pir_db_slice_dev(d_db, nrec, d_dbs)
+    kl = dpf.key_len(logN)
+    for nk in (64, 256):
+        al, ka, kb = _keys(nk, logN, first=9000 + nk)
+        d_work = torch.empty(dpf.pir_workspace_size(nk, logN), dtype=torch.uint8, device=dev)
+        res = []
+        for keys, sliced in ((ka, True), (kb, True), (ka, False)):
+            d_keys = torch.from_numpy(keys.reshape(-1)).to(dev)
+            d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=dev)
+            f = dpf.pir_answer_sliced_dev if sliced else dpf.pir_answer_dev
+            f(d_keys, kl, nk, logN, d_dbs if sliced else d_db, nrec, d_ans, d_work)
+            torch.cuda.synchronize()
+            res.append(d_ans.cpu().numpy().reshape(nk, 32))
+        assert np.array_equal(res[0], res[2])
+        rec = res[0] ^ res[1]
+        for i in range(nk):
+            assert np.array_equal(rec[i], db[int(al[i])]), (nk, i)

@@ -39,10 +39,33 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    auto run = [&]() {
-        CK(hipMemsetAsync(ans, 0, (size_t)nkeys * rec_bytes, 0));
+    // FOLD_MODE=mfma: the matrix-core fold over the bit-sliced DB (32-byte
+    // records), built once here as the PIR server does at load time; its
+    // answers must equal the Four-Russians / direct fold's for every key.
+    const bool mfma = getenv("FOLD_MODE") && getenv("FOLD_MODE")[0] == 'm';
+    void* dbs = nullptr;
+    float slice_ms = 0;
+    std::vector<uint8_t> ref((size_t)nkeys * rec_bytes);
+    if (mfma) {
+        if (rec_bytes != 32) { fprintf(stderr, "mfma mode: 32-byte records only\n"); return 2; }
+        CK(hipMalloc(&dbs, dpfk::pir_sliced_bytes(nrec)));
+        CK(hipEventRecord(e0, 0));
+        CK(dpfk::launch_slice_db((const uint8_t*)db, nrec, (uint8_t*)dbs, 0));
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&slice_ms, e0, e1));
         CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, rec_bytes, nkeys,
                                  (uint32_t*)ans, (uint32_t*)parts, 0));
+        CK(hipMemcpy(ref.data(), ans, ref.size(), hipMemcpyDeviceToHost));
+    }
+    auto run = [&]() {
+        CK(hipMemsetAsync(ans, 0, (size_t)nkeys * rec_bytes, 0));
+        if (mfma)
+            CK(dpfk::launch_pir_fold_sliced((const uint32_t*)bits, wpk, (const uint8_t*)dbs, nrec, nkeys,
+                                            (uint32_t*)ans, (uint32_t*)parts, 0));
+        else
+            CK(dpfk::launch_pir_fold((const uint32_t*)bits, wpk, (const uint8_t*)db, nrec, rec_bytes, nkeys,
+                                     (uint32_t*)ans, (uint32_t*)parts, 0));
     };
     // Clock spin-up: an idle MI355X needs a few hundred ms of load to reach
     // its steady clock.
@@ -66,6 +89,7 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> a((size_t)nkeys * rec_bytes);
     CK(hipMemcpy(a.data(), ans, a.size(), hipMemcpyDeviceToHost));
     int bad = 0;
+    if (mfma) bad += memcmp(ref.data(), a.data(), a.size()) != 0;     // every key vs the LDS fold
     const uint32_t check_keys[2] = {0, nkeys - 1};
     for (uint32_t k : check_keys) {
         std::vector<uint8_t> want(rec_bytes, 0);
@@ -81,10 +105,11 @@ int main(int argc, char** argv) {
 #endif
     const double bytes = (double)nrec * rec_bytes + (double)nkeys * nrec / 8;
     printf("{\"src\": \"%s\", \"nkeys\": %u, \"rec_bytes\": %llu, \"nrec\": %llu, \"kernel\": \"%s\", \"kw\": %u, "
-           "\"col_passes\": %u, \"fold_us\": %.1f, \"GBs\": %.0f, \"db_reads\": %u, \"ok\": %s}\n",
-           FOLD_SRC, nkeys, (unsigned long long)rec_bytes, (unsigned long long)nrec, p.direct ? "direct" : "4r", p.kw,
+           "\"col_passes\": %u, \"fold_us\": %.1f, \"GBs\": %.0f, \"db_reads\": %u, \"slice_db_us\": %.1f, \"ok\": %s}\n",
+           FOLD_SRC, nkeys, (unsigned long long)rec_bytes, (unsigned long long)nrec,
+           mfma ? "mfma" : p.direct ? "direct" : "4r", p.kw,
            p.col_passes, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
-           p.col_passes * ((nkeys + p.keys_per_pass - 1) / p.keys_per_pass), bad ? "false" : "true");
+           p.col_passes * ((nkeys + p.keys_per_pass - 1) / p.keys_per_pass), slice_ms * 1e3, bad ? "false" : "true");
 #ifdef DPF_FOLD_TIMES
     {   // per-wave start / end of the last launch (k_fold4r only)
         std::vector<uint64_t> t(4 * dpfk::kFoldTimesMax);
