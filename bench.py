@@ -388,11 +388,13 @@ def wl_evalfull(c: Ctx) -> dict:
     d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=c.dev)
     d_out = torch.empty(nk * olen, dtype=torch.uint8, device=c.dev)
 
+    # One step = one-shot EvalFull of the resident key bytes (dpf_evalfull_batch_dev):
+    # the T-table tree kernel reads the key bytes itself where every wave owns a
+    # key (no unpack launch); otherwise the keys are unpacked first, inside the step.
     def step(ev):
-        dpf.expand_keys_dev(d_keys, kl, nk, logN, d_work, device=c.local, stream=c.stream)
         if ev:
             ev[0].record(c.stream)
-        dpf.evalfull_expanded_dev(d_work, nk, logN, d_out, device=c.local, stream=c.stream)
+        dpf.evalfull_batch_dev(d_keys, kl, nk, logN, d_out, d_work, device=c.local, stream=c.stream)
         if ev:
             ev[1].record(c.stream)
 
@@ -576,13 +578,11 @@ def wl_split(c: Ctx) -> dict:
     d_keys = torch.from_numpy(ka.reshape(-1)).to(c.dev)
     d_work = torch.empty(dpf.workspace_size(1, logN), dtype=torch.uint8, device=c.dev)
     d_out = torch.empty(part, dtype=torch.uint8, device=c.dev)
-    dpf.expand_keys_dev(d_keys, kl, 1, logN, d_work, device=c.local, stream=c.stream)
 
     def step(ev):
         if ev:
             ev[0].record(c.stream)
-        dpf.evalfull_expanded_dev(d_work, 1, logN, d_out, prefix_bits=pb, prefix=prefix, device=c.local,
-                                  stream=c.stream)
+        dpf.evalfull_subtree_dev(d_keys, kl, 1, logN, pb, prefix, d_out, d_work, device=c.local, stream=c.stream)
         if ev:
             ev[1].record(c.stream)
 

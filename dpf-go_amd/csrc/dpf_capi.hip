@@ -401,6 +401,22 @@ hipError_t run_tree(const TreeWs& w, size_t k0, size_t n, uint32_t stop, uint32_
     return dpfk::launch_evalfull(w.ek + k0 * dpfk::ek_words(stop), n, stop, prefix_bits, prefix, out, stride, st);
 }
 
+// One-shot tree pass from the key bytes in HBM: straight from the bytes when
+// the T-table back end runs a wave-uniform shape (dpfk::evalfull_raw_ok: no
+// unpack launch, d_work untouched), else expand into d_work and run.
+hipError_t tree_from_keys(const uint8_t* d_keys, size_t klen, size_t nk, uint32_t stop, uint32_t prefix_bits,
+                          uint64_t prefix, uint8_t* out, uint64_t stride, void* d_work, hipStream_t st, bool bs,
+                          bool* expanded) {
+    if (!bs && dpfk::evalfull_raw_ok(nk, stop, prefix_bits)) {
+        *expanded = false;
+        return dpfk::launch_evalfull_raw(d_keys, klen, nk, stop, prefix_bits, prefix, out, stride, st);
+    }
+    *expanded = true;
+    const TreeWs w = tree_ws(d_work, nk, stop);
+    hipError_t e = expand_keys(d_keys, klen, nk, stop, w, st, bs);
+    return e != hipSuccess ? e : run_tree(w, 0, nk, stop, prefix_bits, prefix, out, stride, st, bs);
+}
+
 // Pipelined device -> host output of `nchunks` chunks (<= chunk_cap bytes
 // each).  produce(i, dbuf, bytes, host_off) enqueues the kernels writing
 // chunk i into device slot dbuf on d.st.  Kernel i, the PCIe copy of chunk
@@ -486,23 +502,31 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
     HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nk * klen, hipMemcpyHostToDevice, d.st));
     const TreeWs w = tree_ws(d.work.p, nk, stop);
     const bool bs = want_bs();
-    HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, nk, stop, w, d.st, bs));
+    const uint8_t* dk = (const uint8_t*)d.keys.p;
+    uint32_t pb = 0;                                      // one key's output exceeds a chunk: subtree slabs
+    while ((olen >> pb) > kStageBytes) ++pb;
+    // Every chunk straight from the key bytes when each chunk shape allows it
+    // (tree_from_keys), else the keys are expanded once for all chunks.
+    const bool raw = !bs && (olen <= kStageBytes ? dpfk::evalfull_raw_ok(std::min(per, nk), stop, 0) &&
+                                                       (nk % per == 0 || dpfk::evalfull_raw_ok(nk % per, stop, 0))
+                                                 : dpfk::evalfull_raw_ok(1, stop, pb));
+    if (!raw) HIP_TRY(expand_keys(dk, klen, nk, stop, w, d.st, bs));
     if (olen <= kStageBytes) {
         const size_t nch = (nk + per - 1) / per;
         return pipeline_d2h(d, nch, std::min(per, nk) * olen, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
             const size_t k0 = i * per, n = std::min(per, nk - k0);
-            HIP_TRY(run_tree(w, k0, n, stop, 0, 0, dbuf, olen, d.st, bs));
+            if (raw) HIP_TRY(dpfk::launch_evalfull_raw(dk + k0 * klen, klen, n, stop, 0, 0, dbuf, olen, d.st));
+            else HIP_TRY(run_tree(w, k0, n, stop, 0, 0, dbuf, olen, d.st, bs));
             bytes = n * olen;
             off = k0 * olen;
             return DPF_OK;
         }, out, nk * olen);
     }
-    uint32_t pb = 0;                                      // one key's output exceeds a chunk: subtree slabs
-    while ((olen >> pb) > kStageBytes) ++pb;
     const size_t slab = olen >> pb, per_key = (size_t)1 << pb;
     return pipeline_d2h(d, nk * per_key, slab, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
         const size_t k = i / per_key, p = i % per_key;
-        HIP_TRY(run_tree(w, k, 1, stop, pb, p, dbuf, slab, d.st, bs));
+        if (raw) HIP_TRY(dpfk::launch_evalfull_raw(dk + k * klen, klen, 1, stop, pb, p, dbuf, slab, d.st));
+        else HIP_TRY(run_tree(w, k, 1, stop, pb, p, dbuf, slab, d.st, bs));
         bytes = slab;
         off = k * olen + p * slab;
         return DPF_OK;
@@ -847,13 +871,17 @@ int dpf_evalfull_split(const uint8_t* key, size_t klen, uint32_t logN, uint8_t* 
         HIP_TRY(hipMemcpyAsync(d.keys.p, key, klen, hipMemcpyHostToDevice, d.st));
         const TreeWs w = tree_ws(d.work.p, 1, stop);
         const bool bs = want_bs();
-        HIP_TRY(expand_keys((const uint8_t*)d.keys.p, klen, 1, stop, w, d.st, bs));
+        const uint8_t* dk = (const uint8_t*)d.keys.p;
         // This device's subtree (pb, lo), streamed out in sub-slabs (pb + extra, lo * 2^extra + j).
         uint32_t extra = 0;
         while ((slab >> extra) > kStageBytes && pb + extra < stop) ++extra;
         const size_t sub = slab >> extra;
+        const bool raw = !bs && dpfk::evalfull_raw_ok(1, stop, pb + extra);
+        if (!raw) HIP_TRY(expand_keys(dk, klen, 1, stop, w, d.st, bs));
         return pipeline_d2h(d, (size_t)1 << extra, sub, [&](size_t j, uint8_t* dbuf, size_t& bytes, size_t& off) {
-            HIP_TRY(run_tree(w, 0, 1, stop, pb + extra, ((uint64_t)lo << extra) + j, dbuf, sub, d.st, bs));
+            const uint64_t p = ((uint64_t)lo << extra) + j;
+            if (raw) HIP_TRY(dpfk::launch_evalfull_raw(dk, klen, 1, stop, pb + extra, p, dbuf, sub, d.st));
+            else HIP_TRY(run_tree(w, 0, 1, stop, pb + extra, p, dbuf, sub, d.st, bs));
             bytes = sub;
             off = lo * slab + j * sub;
             return DPF_OK;
@@ -869,13 +897,12 @@ int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t klen, siz
         return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
     if (nkeys == 0) return DPF_OK;
     DeviceGuard g(device);
-    const TreeWs w = tree_ws(d_work, nkeys, stop);
     const bool bs = want_bs();
+    bool expanded = false;
     forget_expanded(d_work);
-    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, (hipStream_t)stream, bs));
-    note_expanded(d_work, nkeys, stop, bs);
-    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, d_out, (uint64_t)16 << (stop - prefix_bits),
-                     (hipStream_t)stream, bs));
+    HIP_TRY(tree_from_keys(d_keys, klen, nkeys, stop, prefix_bits, prefix, d_out, (uint64_t)16 << (stop - prefix_bits),
+                           d_work, (hipStream_t)stream, bs, &expanded));
+    if (expanded) note_expanded(d_work, nkeys, stop, bs);
     return DPF_OK;
 }
 
@@ -977,14 +1004,13 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
         return DPF_OK;
     }
     // [tree workspace | selection bits = EvalFull bytes of the subtree | fold partials]
-    const TreeWs w = tree_ws(d_work, nkeys, stop);
     uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
     const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
     const bool bs = want_bs();
+    bool expanded = false;
     forget_expanded(d_work);
-    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st, bs));
-    note_expanded(d_work, nkeys, stop, bs);
-    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st, bs));
+    HIP_TRY(tree_from_keys(d_keys, klen, nkeys, stop, prefix_bits, prefix, bits, per_key, d_work, st, bs, &expanded));
+    if (expanded) note_expanded(d_work, nkeys, stop, bs);
     uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
     HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)bits, per_key / 4, d_db, nrec, 32, (uint32_t)nkeys, (uint32_t*)d_ans,
                                   parts, st));
@@ -1018,14 +1044,13 @@ int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t klen, si
         return DPF_OK;
     }
     // The same workspace and tree pass as dpf_pir_answer_dev; the fold reads the sliced DB.
-    const TreeWs w = tree_ws(d_work, nkeys, stop);
     uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
     const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
     const bool bs = want_bs();
+    bool expanded = false;
     forget_expanded(d_work);
-    HIP_TRY(expand_keys(d_keys, klen, nkeys, stop, w, st, bs));
-    note_expanded(d_work, nkeys, stop, bs);
-    HIP_TRY(run_tree(w, 0, nkeys, stop, prefix_bits, prefix, bits, per_key, st, bs));
+    HIP_TRY(tree_from_keys(d_keys, klen, nkeys, stop, prefix_bits, prefix, bits, per_key, d_work, st, bs, &expanded));
+    if (expanded) note_expanded(d_work, nkeys, stop, bs);
     uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
     HIP_TRY(dpfk::launch_pir_fold_sliced((const uint32_t*)bits, per_key / 4, d_dbs, nrec, (uint32_t)nkeys,
                                          (uint32_t*)d_ans, parts, st));

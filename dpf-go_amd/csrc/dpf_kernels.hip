@@ -82,6 +82,62 @@ __device__ __forceinline__ Blk load_blk(const uint32_t* p) {
     return {a.x, a.y, a.z, a.w};
 }
 
+// Where a thread's key comes from: its expanded records (k_unpack), or --
+// RAW, wave-uniform keys only -- the reference's key bytes themselves
+// (dpf.go:89-92,111-112,137-138,165-167), read with scalar loads of the
+// aligned words around each field and 64-bit funnel shifts, so a one-shot
+// EvalFull needs no unpack launch.  Every load stays inside the dword that
+// holds a key byte, so nothing is read past the batch's last dword.
+struct KeySrc {
+    const uint32_t* ek;    // expanded records of this key
+    const uint32_t* kw;    // RAW: the key batch as 4-byte words (4-byte-aligned base)
+    uint64_t kb, klen;     // RAW: this key's byte offset in the batch; key length
+};
+__device__ __forceinline__ uint32_t funnel(uint32_t a, uint32_t b, uint32_t sh) {
+    return (uint32_t)((((uint64_t)b << 32) | a) >> sh);
+}
+template <bool RAW>
+__device__ __forceinline__ CW key_cw(const KeySrc& k, uint32_t lvl) {
+    if constexpr (!RAW) {
+        return load_cw(k.ek, lvl);
+    } else {
+        const uint64_t o = k.kb + 17 + 18ull * lvl;           // sCW_lvl, tLCW, tRCW (dpf.go:231-233)
+        const uint32_t* p = k.kw + (o >> 2);
+        const uint32_t sh = (uint32_t)(o & 3) * 8;
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+        const uint32_t w5 = sh == 24 ? p[5] : 0u;             // byte o+17 lies in word 5 only then
+        const uint32_t t = funnel(w4, w5, sh);
+        return {{funnel(w0, w1, sh), funnel(w1, w2, sh), funnel(w2, w3, sh), funnel(w3, w4, sh)}, t & 0xffu,
+                (t >> 8) & 0xffu};
+    }
+}
+template <bool RAW>
+__device__ __forceinline__ Blk key_root(const KeySrc& k, uint32_t& t) {
+    if constexpr (!RAW) {
+        t = k.ek[4];
+        return load_blk(k.ek);
+    } else {                                                   // seed k[0:16], t = k[16] (dpf.go:244-246)
+        const uint32_t* p = k.kw + (k.kb >> 2);
+        const uint32_t sh = (uint32_t)(k.kb & 3) * 8;
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+        t = (w4 >> sh) & 0xffu;
+        return {funnel(w0, w1, sh), funnel(w1, w2, sh), funnel(w2, w3, sh), funnel(w3, w4, sh)};
+    }
+}
+template <bool RAW>
+__device__ __forceinline__ Blk key_fcw(const KeySrc& k, uint32_t stop) {
+    if constexpr (!RAW) {
+        return load_blk(k.ek + 8 + 8 * stop);
+    } else {                                                   // final CW = k[len-16:] (dpf.go:206,219)
+        const uint64_t o = k.kb + k.klen - 16;
+        const uint32_t* p = k.kw + (o >> 2);
+        const uint32_t sh = (uint32_t)(o & 3) * 8;
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3];
+        const uint32_t w4 = sh ? p[4] : 0u;
+        return {funnel(w0, w1, sh), funnel(w1, w2, sh), funnel(w2, w3, sh), funnel(w3, w4, sh)};
+    }
+}
+
 // prg (dpf.go:59-69) plus the parent's CW correction (dpf.go:230-238).
 // The two independent MMOs of a PRG call (or of a leaf pair), written as two
 // plain mmo1 calls so the scheduler interleaves them freely: 98.9 G blocks/s
@@ -152,7 +208,7 @@ __device__ __forceinline__ Blk leaf_fix(Blk o, uint32_t t, Blk fcw) {
 struct Ctx {
     const uint8_t* tab;
     uint32_t lo;
-    const uint32_t* ek;
+    KeySrc ks;
     Blk fcw;
     uint8_t* outp;      // leaf mode: 16-byte leaf cursor
     uint4* nseed;       // node mode: seed cursor
@@ -216,12 +272,12 @@ __device__ __forceinline__ Blk bsel(bool b, const Blk& x, const Blk& y) {
 // two inlined copies: the tree kernel's innermost loop must fit the
 // instruction cache (64 KiB per two CUs).  Fully inlined, the PAIR path's
 // loop body was ~85 KiB of code (22 AES-MMO bodies).
-template <bool B>
+template <bool B, bool RAW>
 __device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& n, uint8_t* p) {
-    CW cw = load_cw(c.ek, lvl);
+    CW cw = key_cw<RAW>(c.ks, lvl);
     Node L, R;
     expand<B>(c.tab, c.lo, n, cw, L, R);
-    CW cw1 = load_cw(c.ek, lvl + 1);
+    CW cw1 = key_cw<RAW>(c.ks, lvl + 1);
     Blk o0 = {}, o1 = {}, o2, o3;
     // Only the pending child stays live through the first iteration (a
     // select of L or R at the top of each iteration kept both live: 5 more
@@ -257,7 +313,7 @@ __device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& 
 // D levels down instead: the frontier a batched Eval continues from.
 // B: batched AES rounds (aes_ttable.hpp aes2_rounds) where the registers
 // allow it: the one-key-per-wave kernels.
-template <int DMAX, int D, bool NODES, bool PAIR, bool B>
+template <int DMAX, int D, bool NODES, bool PAIR, bool B, bool RAW = false>
 __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
     if constexpr (PAIR && D == 3) {
         // Lane pairs write whole 128-B lines.  Lanes 2i and 2i+1 own adjacent
@@ -269,7 +325,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         // apart left ~4 MiB of half-written lines per XCD (its whole L2) and
         // made WRITE_SIZE 1.26x the output.  Leaves are unchanged, only which
         // lane computes them.
-        CW cw = load_cw(c.ek, lvl0 + DMAX - 3);
+        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - 3);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
         const bool odd = (threadIdx.x & 1u) != 0;
@@ -279,7 +335,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         const Node second = sel(odd, R, got);
 #pragma nounroll
         for (int h = 0; h < 2; ++h) {   // one code copy of leaves4 (instruction cache)
-            leaves4<B>(c, lvl0 + DMAX - 2, cur, c.outp + (h == 0 ? (odd ? 64 - sub : 0) : (odd ? 64 : sub)));
+            leaves4<B, RAW>(c, lvl0 + DMAX - 2, cur, c.outp + (h == 0 ? (odd ? 64 - sub : 0) : (odd ? 64 : sub)));
             prio_step<DMAX>(c);
             cur = second;
         }
@@ -295,17 +351,17 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
     } else if constexpr (D == 2 && !NODES) {
         // Bottom two levels at once: 4 leaves = 64 contiguous bytes stored back
         // to back (subtrees too shallow or lanes of different keys for PAIR).
-        leaves4<B>(c, lvl0 + DMAX - 2, n, c.outp);
+        leaves4<B, RAW>(c, lvl0 + DMAX - 2, n, c.outp);
         prio_step<DMAX>(c);
         c.outp += 64;
     } else if constexpr (D == 2 && NODES) {
         // Bottom two levels of a frontier at once: 4 seeds = 64 contiguous
         // bytes and their 4 t bytes as one 32-bit store (one byte store per
         // node made the NODES pass write 2.2x its 17 B per node).
-        CW cw = load_cw(c.ek, lvl0 + DMAX - 2);
+        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - 2);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
-        CW cw1 = load_cw(c.ek, lvl0 + DMAX - 1);
+        CW cw1 = key_cw<RAW>(c.ks, lvl0 + DMAX - 1);
         Node q[4];
         expand<B>(c.tab, c.lo, L, cw1, q[0], q[1]);
         expand<B>(c.tab, c.lo, R, cw1, q[2], q[3]);
@@ -317,7 +373,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         c.nt += 4;
         prio_step<DMAX>(c);
     } else if constexpr (D == 1) {
-        CW cw = load_cw(c.ek, lvl0 + DMAX - 1);
+        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - 1);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
         if constexpr (NODES) {
@@ -331,7 +387,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
             c.outp += 32;
         }
     } else {
-        CW cw = load_cw(c.ek, lvl0 + DMAX - D);
+        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - D);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
         // The right child is the only node live across the left subtree.
@@ -339,7 +395,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         const Node pend = R;
 #pragma nounroll
         for (int side = 0; side < 2; ++side) {
-            dfs<DMAX, D - 1, NODES, PAIR, B>(c, lvl0, ch);
+            dfs<DMAX, D - 1, NODES, PAIR, B, RAW>(c, lvl0, ch);
             ch = pend;
         }
     }
@@ -377,11 +433,13 @@ __global__ void k_unpack(const uint8_t* __restrict__ keys, uint64_t key_len, uin
 // written at out + key*out_stride + (u mod 2^units_log) * 16 * 2^D.
 // NODES: the same walk, but the 2^D nodes at level ltop + D are written to
 // (uint4*)out / out_t at [key*out_stride + (u mod 2^units_log) * 2^D].
-template <int D, bool UNIFORM, bool NODES>
+template <int D, bool UNIFORM, bool NODES, bool RAW = false>
 __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                         uint64_t nunits, uint32_t units_log, uint32_t ltop,
                                                         uint64_t sub_base, uint8_t* __restrict__ out,
-                                                        uint8_t* __restrict__ out_t, uint64_t out_stride) {
+                                                        uint8_t* __restrict__ out_t, uint64_t out_stride,
+                                                        uint64_t klen = 0, uint64_t kboff = 0) {
+    static_assert(!RAW || (UNIFORM && !NODES), "raw keys: wave-uniform leaf launches only");
 #ifdef DPF_WAVE_TIMES
     const uint64_t t_start = wall_clock64();
 #endif
@@ -393,27 +451,28 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
     const uint64_t local = u & ((1ull << units_log) - 1);
     const uint64_t sub = sub_base + local;
-    const uint32_t* ek = ekeys + key * ((uint64_t)(stop + 2) * 8);
-
     Ctx c;
+    if constexpr (RAW) {
+        c.ks = {nullptr, ekeys, kboff + key * klen, klen};   // ekeys: the raw key batch, 4-byte-aligned base
+    } else {
+        c.ks = {ekeys + key * ((uint64_t)(stop + 2) * 8), nullptr, 0, 0};
+    }
     c.groups = 0;
 #if DPF_PRIO_STEPS
     __builtin_amdgcn_s_setprio(3);
 #endif
     c.tab = reinterpret_cast<const uint8_t*>(s_tab);
     c.lo = (threadIdx.x & 31u) * 4u;
-    c.ek = ek;
     if constexpr (NODES) {
         c.nseed = reinterpret_cast<uint4*>(out) + key * out_stride + (local << D);
         c.nt = out_t + key * out_stride + (local << D);
     } else {
-        c.fcw = load_blk(ek + 8 + 8 * stop);
+        c.fcw = key_fcw<RAW>(c.ks, stop);
         c.outp = out + key * out_stride + local * (16ull << D);
     }
 
     Node n;
-    n.s = load_blk(ek);
-    n.t = ek[4];
+    n.s = key_root<RAW>(c.ks, n.t);
     uint32_t lvl = 0;
     if constexpr (UNIFORM) {
         // Shared walk: when the whole workgroup (B = 2^W threads) evaluates
@@ -432,7 +491,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
                 const uint64_t subj = (sub - threadIdx.x) + ((uint64_t)threadIdx.x << (W - 6));
                 Node m = n;
                 for (uint32_t i = 0; i < l1; ++i) {
-                    CW cw = load_cw(ek, i);
+                    CW cw = key_cw<RAW>(c.ks, i);
                     walk_step<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
                 }
                 uint32_t* f = s_front + 5 * threadIdx.x;
@@ -446,14 +505,14 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
         }
     }
     for (uint32_t i = lvl; i < ltop; ++i) {
-        CW cw = load_cw(ek, i);
+        CW cw = key_cw<RAW>(c.ks, i);
         walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
     // Lane pairs share a key when a wave owns one key (UNIFORM): whole-line
     // leaf stores (dfs PAIR).  DPF_PAIR_STORES=0 builds the r02 half-line
     // stores for A/B runs.
     constexpr bool kPair = DPF_PAIR_STORES && UNIFORM && !NODES && D >= 3;
-    dfs<D, D, NODES, kPair, UNIFORM>(c, ltop, n);
+    dfs<D, D, NODES, kPair, UNIFORM, RAW>(c, ltop, n);
 #ifdef DPF_WAVE_TIMES
     // Measurement build only (tools/wave_times.hip): per wave, start / end
     // (wall clock) and the hardware ids of the CU it ran on.
@@ -533,10 +592,32 @@ __device__ __forceinline__ uint8_t eval_bit(Blk o, uint64_t x) {
     const uint32_t w = (b >> 5) == 0 ? o.c0 : (b >> 5) == 1 ? o.c1 : (b >> 5) == 2 ? o.c2 : o.c3;
     return (uint8_t)((w >> (b & 31)) & 1u);
 }
-__device__ __forceinline__ void eval_pair(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
-                                          const uint64_t* __restrict__ xs, uint64_t nq, uint64_t pts_per_key,
-                                          const uint4* __restrict__ fseed, const uint8_t* __restrict__ ft, uint32_t L,
-                                          uint8_t* __restrict__ out, const uint32_t* s_tab, uint64_t q0) {
+struct PairIn {
+    uint64_t x0, x1;
+    Node n0, n1;
+};
+// The pair's points and start nodes (frontier gathers): issued before the
+// workgroup fills its table, so their HBM latency overlaps the fill
+// (DPF_EVAL_EARLY; the first pair of every thread).
+__device__ __forceinline__ PairIn eval_pair_in(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
+                                               const uint64_t* __restrict__ xs, uint64_t nq, uint64_t pts_per_key,
+                                               const uint4* __restrict__ fseed, const uint8_t* __restrict__ ft,
+                                               uint32_t L, uint64_t q0) {
+    const uint64_t qa = q0 < nq ? q0 : nq - 1;
+    const uint64_t q1 = qa + 1 < nq ? qa + 1 : qa;
+    const uint64_t key0 = qa / pts_per_key, key1 = q1 / pts_per_key;
+    const uint64_t rec = (uint64_t)(stop + 2) * 8;
+    PairIn p;
+    p.x0 = xs[qa];
+    p.x1 = xs[q1];
+    p.n0 = eval_start(ekeys + key0 * rec, key0, p.x0, logN, fseed, ft, L);
+    p.n1 = eval_start(ekeys + key1 * rec, key1, p.x1, logN, fseed, ft, L);
+    return p;
+}
+__device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
+                                               uint64_t nq, uint64_t pts_per_key, const uint4* __restrict__ fseed,
+                                               uint32_t L, uint8_t* __restrict__ out, const uint32_t* s_tab,
+                                               uint64_t q0, PairIn p) {
     const bool two = q0 + 1 < nq;
     const uint64_t q1 = two ? q0 + 1 : q0;
     const uint64_t key0 = q0 / pts_per_key, key1 = q1 / pts_per_key;
@@ -545,28 +626,28 @@ __device__ __forceinline__ void eval_pair(const uint32_t* __restrict__ ekeys, ui
     const uint32_t* ek1 = ekeys + key1 * rec;
     const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
     const uint32_t lo = (threadIdx.x & 31u) * 4u;
-    const uint64_t x0 = xs[q0], x1 = xs[q1];
-    Node n0 = eval_start(ek0, key0, x0, logN, fseed, ft, L);
-    Node n1 = eval_start(ek1, key1, x1, logN, fseed, ft, L);
     for (uint32_t i = fseed != nullptr ? L : 0; i < stop; ++i) {
         const CW cw0 = load_cw(ek0, i), cw1 = load_cw(ek1, i);
-        walk_step2<DPF_EVAL_BATCH>(tab, lo, n0, cw0, path_bit(x0, logN - 1 - i), n1, cw1, path_bit(x1, logN - 1 - i));
+        walk_step2<DPF_EVAL_BATCH>(tab, lo, p.n0, cw0, path_bit(p.x0, logN - 1 - i), p.n1, cw1,
+                                   path_bit(p.x1, logN - 1 - i));
     }
     Blk o0, o1;
-    mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n0.s, o0, KeyFixed<false>{}, n1.s, o1);
-    o0 = leaf_fix(o0, n0.t, load_blk(ek0 + 8 + 8 * stop));
-    o1 = leaf_fix(o1, n1.t, load_blk(ek1 + 8 + 8 * stop));
-    out[q0] = eval_bit(o0, x0);
-    if (two) out[q1] = eval_bit(o1, x1);
+    mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, p.n0.s, o0, KeyFixed<false>{}, p.n1.s, o1);
+    o0 = leaf_fix(o0, p.n0.t, load_blk(ek0 + 8 + 8 * stop));
+    o1 = leaf_fix(o1, p.n1.t, load_blk(ek1 + 8 + 8 * stop));
+    out[q0] = eval_bit(o0, p.x0);
+    if (two) out[q1] = eval_bit(o1, p.x1);
 }
 
+#ifndef DPF_EVAL_EARLY
+#define DPF_EVAL_EARLY 1
+#endif
 __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                      uint32_t logN, const uint64_t* __restrict__ xs, uint64_t nq,
                                                      uint64_t pts_per_key, const uint4* __restrict__ fseed,
                                                      const uint8_t* __restrict__ ft, uint32_t L,
                                                      uint8_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-    fill_table(s_tab);
     // Grid-stride loop.  launch_eval launches one thread per query pair
     // (iters = 1); DPF_EVAL_STRIDE=1 caps the grid at the resident
     // workgroups so each fills its 64 KiB table once, with the issue priority
@@ -576,12 +657,28 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
     const uint64_t stride = 2 * (uint64_t)gridDim.x * blockDim.x;
     const uint64_t first = 2 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
     const uint64_t iters = first < nq ? (nq - first + stride - 1) / stride : 0;
+#if DPF_EVAL_EARLY
+    // The first pair's points and frontier nodes are requested before the
+    // table fill (a short-lived wave otherwise waits out their HBM latency
+    // after it).
+    PairIn p0{};
+    if (iters) p0 = eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, first);
+#endif
+    fill_table(s_tab);
     __builtin_amdgcn_s_setprio(3);
-    for (uint64_t it = 0; it < iters; ++it) {
+#if DPF_EVAL_EARLY
+    if (iters) eval_pair_walk(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, first, p0);
+    const uint64_t it0 = 1;
+#else
+    const uint64_t it0 = 0;
+#endif
+    for (uint64_t it = it0; it < iters; ++it) {
         if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
         else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
-        eval_pair(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, out, s_tab, first + it * stride);
+        const uint64_t q0 = first + it * stride;
+        eval_pair_walk(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, q0,
+                       eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0));
     }
 }
 
@@ -745,6 +842,50 @@ static hipError_t launch_tree(const uint32_t* ek, uint64_t nkeys, uint32_t stop,
         default: DPF_LAUNCH(7);
     }
 #undef DPF_LAUNCH
+}
+
+// One-shot EvalFull straight from the key bytes (RAW): only where every wave
+// owns one key (the shape launch_tree would pick has >= 64 threads per key)
+// and DPF_RAW_KEYS is not 0 (measurement switch).  Any key alignment: the
+// kernel reads from the 4-byte-aligned base below `keys`.
+bool evalfull_raw_ok(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits) {
+    static const bool on = [] {
+        const char* e = getenv("DPF_RAW_KEYS");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || nkeys == 0 || prefix_bits > stop) return false;
+    const uint32_t span = stop - prefix_bits;
+    const TreeShape sh = pick_shape(span, nkeys, false, prefix_bits);
+    return span - sh.d >= 6;                             // units_log >= 6: UNIFORM
+}
+
+hipError_t launch_evalfull_raw(const uint8_t* keys, uint64_t klen, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
+                               uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st) {
+    const uint32_t span = stop - prefix_bits;
+    const TreeShape sh = pick_shape(span, nkeys, false, prefix_bits);
+    const uint32_t d = sh.d, ltop = stop - d, units_log = ltop - prefix_bits;
+    if (units_log < 6) return hipErrorInvalidValue;
+    const uint64_t nunits = nkeys << units_log, sub_base = prefix << units_log;
+    const uint64_t blocks = (nunits + sh.block - 1) / sh.block;
+    // Aligned base below the batch, the batch's offset from it in kboff.
+    const uint64_t kboff = (uintptr_t)keys & 3;
+    const uint32_t* kw = reinterpret_cast<const uint32_t*>(keys - kboff);
+#define DPF_RAW(DD)                                                                                                  \
+    hipLaunchKernelGGL((k_evalfull<DD, true, false, true>), dim3((uint32_t)blocks), dim3(sh.block), 0, st, kw, stop, \
+                       nunits, units_log, ltop, sub_base, out, nullptr, out_stride, klen, kboff);                   \
+    break
+    switch (d) {
+        case 0: DPF_RAW(0);
+        case 1: DPF_RAW(1);
+        case 2: DPF_RAW(2);
+        case 3: DPF_RAW(3);
+        case 4: DPF_RAW(4);
+        case 5: DPF_RAW(5);
+        case 6: DPF_RAW(6);
+        default: DPF_RAW(7);
+    }
+#undef DPF_RAW
+    return hipGetLastError();
 }
 
 hipError_t launch_nodes(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t depth, uint32_t prefix_bits,

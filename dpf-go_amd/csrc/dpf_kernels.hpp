@@ -35,6 +35,13 @@ hipError_t launch_unpack(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, 
 hipError_t launch_evalfull(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
                            uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st);
 
+// The same from the key bytes themselves ([nkeys][klen], the reference's
+// layout, any alignment), no unpack launch: only where evalfull_raw_ok()
+// (every wave owns one key).
+bool evalfull_raw_ok(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits);
+hipError_t launch_evalfull_raw(const uint8_t* keys, uint64_t klen, uint64_t nkeys, uint32_t stop, uint32_t prefix_bits,
+                               uint64_t prefix, uint8_t* out, uint64_t out_stride, hipStream_t st);
+
 // The 2^(depth - prefix_bits) nodes at level `depth` below prefix node
 // (prefix_bits, prefix) of every key: seeds (16 B) at seeds + (key * stride
 // + j) * 16 and t bytes at ts + key * stride + j.

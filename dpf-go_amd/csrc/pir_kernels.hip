@@ -640,10 +640,10 @@ hipError_t fold_pass(const FoldArgs& a, bool direct, int kw, uint32_t* ans, uint
 // selection words 8S + 4h .. +3 (one dwordx4 each, both coalesced): K-block
 // t < 4 of super-group S is record groups t (h = 0) and 4 + t (h = 1).
 // Word -> FP4 operand in registers, nibble i of dword d = record 4i + d:
-//   DB    d0 = x & 0x1..  (0.5)  d1 = x & 0x2.. (1.0)  d2 = x & 0x4.. (2.0)
-//         d3 = (x >> 1) & 0x4.. (2.0)                       5 VALU per word
-//   keys  d0 = (s << 2) & 0x4.. (2.0)  d1 = s & 0x2.. (1.0)
-//         d2 = (s >> 2) & 0x1.. (0.5)  d3 = (s >> 3) & 0x1.. (0.5)
+//   one side  d0 = x & 0x1..  (0.5)  d1 = x & 0x2.. (1.0)  d2 = x & 0x4.. (2.0)
+//             d3 = (x >> 1) & 0x4.. (2.0)                       5 VALU per word
+//   the other d0 = (s << 2) & 0x4.. (2.0)  d1 = s & 0x2.. (1.0)
+//             d2 = (s >> 2) & 0x1.. (0.5)  d3 = (s >> 3) & 0x1.. (0.5)   7 VALU
 // so every nonzero product is exactly 1 with unit (E8M0 127) scales.
 //
 // Mapping.  A wave covers MT key tiles (32 keys) x NT bit tiles (32 bit
@@ -655,7 +655,14 @@ hipError_t fold_pass(const FoldArgs& a, bool direct, int kw, uint32_t* ans, uint
 typedef int fold_v8i __attribute__((ext_vector_type(8)));
 typedef float fold_v16f __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ fold_v8i fp4_db(uint32_t x) {
+// Which side takes the cheap 5-op expansion (ANDs + one shift; weights 0.5,
+// 1, 2, 2) and which the 7-op one (weights 2, 1, 0.5, 0.5): the selection
+// side is expanded once per MT x NT tile group for NT tiles, the DB side for
+// MT, so the side shared by fewer MFMAs should be the cheap one.
+#ifndef DPF_FOLD_SEL_CHEAP
+#define DPF_FOLD_SEL_CHEAP 1
+#endif
+__device__ __forceinline__ fold_v8i fp4_w5(uint32_t x) {     // weights 0.5, 1, 2, 2
     fold_v8i r;
     r[0] = (int)(x & 0x11111111u);
     r[1] = (int)(x & 0x22222222u);
@@ -664,7 +671,7 @@ __device__ __forceinline__ fold_v8i fp4_db(uint32_t x) {
     r[4] = r[5] = r[6] = r[7] = 0;
     return r;
 }
-__device__ __forceinline__ fold_v8i fp4_sel(uint32_t s) {
+__device__ __forceinline__ fold_v8i fp4_w7(uint32_t s) {     // weights 2, 1, 0.5, 0.5
     fold_v8i r;
     r[0] = (int)((s << 2) & 0x44444444u);
     r[1] = (int)(s & 0x22222222u);
@@ -673,41 +680,43 @@ __device__ __forceinline__ fold_v8i fp4_sel(uint32_t s) {
     r[4] = r[5] = r[6] = r[7] = 0;
     return r;
 }
+__device__ __forceinline__ fold_v8i fp4_db(uint32_t x) { return DPF_FOLD_SEL_CHEAP ? fp4_w7(x) : fp4_w5(x); }
+__device__ __forceinline__ fold_v8i fp4_sel(uint32_t s) { return DPF_FOLD_SEL_CHEAP ? fp4_w5(s) : fp4_w7(s); }
 __device__ __forceinline__ uint32_t u4w(const uint4& v, int t) { return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w; }
 
 constexpr int kFoldFp4 = 4;         // cbsz / blgp format code of e2m1
 constexpr int kE8M0One = 127;       // block scale 2^0
 
-// Selection words reach the waves through LDS: per block of kSelSG
-// super-groups the workgroup copies each key's 128-byte span (one whole line
-// per key, coalesced) into a padded row, and the next block's lines are in
-// flight in registers while this one is folded.  (Loaded straight into the
-// operand lanes, 16 B per lane from 32 rows 2 MiB apart, the fold fetched
-// ~1.6x its bytes and ran at a third of the HBM rate: profiles/r04/fold_v1.)
-constexpr int kSelSG = 4;                       // super-groups per staged block: 128 B per key
-constexpr int kSelRow = kSelSG * 8 + 4;         // words per staged row (+4: conflict-free ds_read_b128)
-
-template <int MT, int NT>
+// Selection words reach the waves through LDS: per block of SG super-groups
+// the workgroup copies each key's SG*32-byte span (coalesced) into a padded
+// row, and the next block's selection words and DB pieces are in flight in
+// registers while this block is folded (block-level double buffering: a
+// super-group of MFMA work is ~0.2-0.4 us per wave, shorter than the HBM
+// latency under load).  Loaded straight into the operand lanes, 16 B per
+// lane from 32 rows 2 MiB apart, the fold fetched ~1.6x its bytes and ran at
+// a third of the HBM rate (profiles/r04/fold_v1).
+template <int MT, int NT, int SG>
 __global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words) {
     constexpr int NW = 8 / NT;
     constexpr int kRows = 32 * MT;
-    constexpr int kPieces = kRows * (kSelSG * 8 / 4);          // uint4 pieces per staged block
+    constexpr int kRow = SG * 8 + 4;                           // words per staged row (+4: conflict-free b128 reads)
+    constexpr int kPieces = kRows * (SG * 2);                  // uint4 pieces per staged block
     constexpr int kPer = (kPieces + 64 * NW - 1) / (64 * NW);  // per thread
-    __shared__ __attribute__((aligned(16))) uint32_t s_sel[kRows * kSelRow];
+    __shared__ __attribute__((aligned(16))) uint32_t s_sel[kRows * kRow];
     zero_answers(zero, zero_words);
     const uint32_t l = threadIdx.x & 63, h = l >> 5, r = l & 31;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t s0 = (uint64_t)blockIdx.x * sg_per_block;
     const uint64_t s1 = s0 + sg_per_block < nsg ? s0 + sg_per_block : nsg;
     if (s0 >= s1) return;                                       // uniform over the workgroup
-    // Staging role: piece p = threadIdx.x + i*64*NW is row p/8, 16 bytes p%8.
+    // Staging role: piece p = threadIdx.x + i*64*NW is row p/(2SG), 16 bytes p%(2SG).
     auto load_sel = [&](uint64_t sb, uint4 (&v)[kPer]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const uint32_t p = threadIdx.x + (uint32_t)i * 64 * NW;
-            const uint32_t row = p >> 3, q = p & 7;
+            const uint32_t row = p / (2 * SG), q = p % (2 * SG);
             const uint64_t word = sb * 8 + 4 * q;
             const bool ok = p < (uint32_t)kPieces && row < nkeys && word + 4 <= wpk;
             const uint4 x = *reinterpret_cast<const uint4*>(bits + (uint64_t)(ok ? row : 0) * wpk + (ok ? word : 0));
@@ -719,12 +728,17 @@ __global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_
         for (int i = 0; i < kPer; ++i) {
             const uint32_t p = threadIdx.x + (uint32_t)i * 64 * NW;
             if (p < (uint32_t)kPieces)
-                *reinterpret_cast<uint4*>(&s_sel[(p >> 3) * kSelRow + 4 * (p & 7)]) = v[i];
+                *reinterpret_cast<uint4*>(&s_sel[(p / (2 * SG)) * kRow + 4 * (p % (2 * SG))]) = v[i];
         }
     };
-    auto load_db = [&](uint64_t S, uint4 (&B)[NT]) __attribute__((always_inline)) {
+    // DB pieces of a whole block (clamped past the range; never folded).
+    auto load_db = [&](uint64_t sb, uint4 (&B)[SG][NT]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j) B[j] = dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h];
+        for (int sl = 0; sl < SG; ++sl) {
+            const uint64_t S = sb + sl < s1 ? sb + sl : s1 - 1;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) B[sl][j] = dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h];
+        }
     };
     fold_v16f acc[MT][NT];
 #pragma unroll
@@ -733,16 +747,12 @@ __global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[m][j][e] = 0.0f;
-    uint4 sv[kPer];
-    load_sel(s0, sv);
-    uint4 B0[NT], B1[NT];
-    load_db(s0, B0);
     // One super-group: 4 K-blocks of 64 records x MT x NT MFMAs.
-    auto fold_sg = [&](uint32_t sl, const uint4 (&B)[NT]) __attribute__((always_inline)) {
+    auto fold_sg = [&](int sl, const uint4 (&B)[NT]) __attribute__((always_inline)) {
         uint4 A[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-            A[m] = *reinterpret_cast<const uint4*>(&s_sel[(32 * m + r) * kSelRow + 8 * sl + 4 * h]);
+            A[m] = *reinterpret_cast<const uint4*>(&s_sel[(32 * m + r) * kRow + 8 * sl + 4 * h]);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             fold_v8i bo[NT];
@@ -758,29 +768,31 @@ __global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_
             }
         }
     };
-    for (uint64_t sb = s0; sb < s1; sb += kSelSG) {
+    uint4 sv[kPer];
+    uint4 BA[SG][NT], BB[SG][NT];
+    load_sel(s0, sv);
+    load_db(s0, BA);
+    // One staged block: its selection rows to LDS, the next block's loads
+    // issued, then its super-groups folded.
+    auto block = [&](uint64_t sb, const uint4 (&Bc)[SG][NT], uint4 (&Bn)[SG][NT]) __attribute__((always_inline)) {
         fold_prio(sb - s0, s1 - s0);
         __syncthreads();                                        // previous block's operand reads are done
         store_sel(sv);
         __syncthreads();
-        const uint64_t nb = sb + kSelSG < s1 ? sb + kSelSG : sb;   // next block in flight (clamped)
+        const uint64_t nb = sb + SG < s1 ? sb + SG : sb;        // next block (clamped)
         load_sel(nb, sv);
-        const uint32_t n = s1 - sb < (uint64_t)kSelSG ? (uint32_t)(s1 - sb) : (uint32_t)kSelSG;
-        // Super-groups of the block in pairs: the DB pieces ping-pong, the
-        // next one in flight while this one folds.
-        for (uint32_t sl = 0; sl < n; sl += 2) {
-            const uint64_t S = sb + sl;
-            load_db(S + 1 < s1 ? S + 1 : S, B1);
-            fold_sg(sl, B0);
-            if (sl + 1 < n) {
-                load_db(S + 2 < s1 ? S + 2 : S + 1, B0);
-                fold_sg(sl + 1, B1);
-            } else {
+        load_db(nb, Bn);
+        const uint64_t n = s1 - sb;
 #pragma unroll
-                for (int j = 0; j < NT; ++j) B0[j] = B1[j];
-            }
-        }
+        for (int sl = 0; sl < SG; ++sl)
+            if ((uint64_t)sl < n) fold_sg(sl, Bc[sl]);
+    };
+    uint64_t sb = s0;
+    for (; sb + SG < s1; sb += 2 * SG) {
+        block(sb, BA, BB);
+        block(sb + SG, BB, BA);
     }
+    if (sb < s1) block(sb, BA, BB);
     // Parities -> answer words: parts[block][key][8] (word = bit tile).
     constexpr uint32_t pkeys = 32 * MT;
 #pragma unroll
@@ -842,7 +854,7 @@ hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipSt
 }
 
 namespace {
-template <int MT, int NT>
+template <int MT, int NT, int SG>
 hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
                           uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st) {
     constexpr int NW = 8 / NT;
@@ -851,18 +863,24 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
     // them for a second round at 3 or 1 resident per CU.)
     static int per_cu = [] {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_mfma<MT, NT>, 64 * NW, 0) != hipSuccess || n < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_mfma<MT, NT, SG>, 64 * NW, 0) != hipSuccess || n < 1)
             n = 1;
         return n;
     }();
     uint64_t spb;
-    split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, kSelSG, blocks, spb);
-    hipLaunchKernelGGL((k_fold_mfma<MT, NT>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+    split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
+    hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
                        reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words);
     return hipGetLastError();
 }
 }  // namespace
 
+#ifndef DPF_FOLD_NT4
+#define DPF_FOLD_NT4 1   // bit tiles per wave at 65-128 keys (8 / NT waves per workgroup)
+#endif
+#ifndef DPF_FOLD_NT8
+#define DPF_FOLD_NT8 1   // ... at 129-256 keys
+#endif
 hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
                                   uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
     if (nkeys == 0) return hipSuccess;
@@ -877,10 +895,10 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
         uint64_t blocks = 0;
         uint32_t mt;
         hipError_t e;
-        if (nk <= 32) e = launch_mfma_mt<1, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 1;
-        else if (nk <= 64) e = launch_mfma_mt<2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 2;
-        else if (nk <= 128) e = launch_mfma_mt<4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 4;
-        else e = launch_mfma_mt<8, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 8;
+        if (nk <= 32) e = launch_mfma_mt<1, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 1;
+        else if (nk <= 64) e = launch_mfma_mt<2, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 2;
+        else if (nk <= 128) e = launch_mfma_mt<4, DPF_FOLD_NT4, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 4;
+        else e = launch_mfma_mt<8, DPF_FOLD_NT8, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 8;
         if (e != hipSuccess) return e;
         const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
         hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk, 32 * mt,

@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_fold.py -v --timeout 120 --
     > "$OUT/tests.log" 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 "$OUT/tests.log"
 [ $rc -le 1 ] || exit $rc
-for b in 1 4 16 32 64 128 256 512; do
+for b in 1 4 8 16 32 64 128 256 512; do
   for m in lds mfma; do
     FOLD_MODE=$m timeout -k 10 120 tools/fold_bench $b 32 24 >> "$OUT/fold_bench.jsonl" 2>> "$OUT/fold_bench.err"
     rc=$?; [ $rc -le 1 ] || { echo "fold_bench $m $b rc=$rc"; exit $rc; }
