@@ -632,13 +632,31 @@ def split_api_rate(c: Ctx, key: bytes, logN: int, reps: int = 3) -> dict:
 
 
 def pir_setup(c: Ctx, W: int):
-    """This rank's DB slice in HBM (the same synthetic DB on every run)."""
+    """This rank's DB slice in HBM (the same synthetic DB on every run), in
+    the layout the fold reads: bit-sliced for the matrix-core fold (built
+    once on the device, like a server loading its DB; not timed per step),
+    row-major for the LDS fold (--pir-fold lds)."""
     from dpf import synth, shard
+    torch, dpf = c.torch, c.dpf
     logN = c.args.pir_logN
     nrec = 1 << logN
     lo, hi = shard.db_slice(nrec, logN, W, c.rank)
     db = synth.db_bytes(hi * 32)[lo * 32:]                    # this rank's slice of the synthetic DB
-    return c.torch.from_numpy(db).to(c.dev), lo, hi
+    d_db = torch.from_numpy(db).to(c.dev)
+    c.pir_layout = {"fold": c.args.pir_fold}
+    if c.args.pir_fold == "mfma":
+        d_dbs = torch.empty(dpf.pir_db_sliced_size(hi - lo), dtype=torch.uint8, device=c.dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(c.stream)
+        dpf.pir_db_slice_dev(d_db, hi - lo, d_dbs, device=c.local, stream=c.stream)
+        ev1.record(c.stream)
+        torch.cuda.synchronize(c.dev)
+        c.pir_layout.update({"db_layout": "bit-sliced (dpf_pir_db_slice_dev, once per DB load)",
+                             "db_slice_ms": round(ev0.elapsed_time(ev1), 3)})
+        del d_db
+        return d_dbs, lo, hi
+    c.pir_layout["db_layout"] = "row-major"
+    return d_db, lo, hi
 
 
 def pir_time(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int, warmup: int):
@@ -667,8 +685,9 @@ def pir_time(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int, warmup
     def step(ev):
         if ev:
             ev[0].record(c.stream)
-        dpf.pir_answer_dev(d_keys, kl, nk, logN, d_db, hi - lo, d_ans, d_work, prefix_bits=pb, prefix=prefix,
-                           device=c.local, stream=c.stream)
+        answer = dpf.pir_answer_sliced_dev if c.args.pir_fold == "mfma" else dpf.pir_answer_dev
+        answer(d_keys, kl, nk, logN, d_db, hi - lo, d_ans, d_work, prefix_bits=pb, prefix=prefix,
+               device=c.local, stream=c.stream)
         if ev:
             ev[1].record(c.stream)
         if c.world > 1:
@@ -716,7 +735,10 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
     def fold(ev):
         if ev:
             ev[0].record(c.stream)
-        dpf.xor_fold_dev(d_bits, per_key, nk, d_db, hi - lo, 32, d_ans, d_fw, device=c.local, stream=c.stream)
+        if c.args.pir_fold == "mfma":
+            dpf.xor_fold_sliced_dev(d_bits, per_key, nk, d_db, hi - lo, d_ans, d_fw, device=c.local, stream=c.stream)
+        else:
+            dpf.xor_fold_dev(d_bits, per_key, nk, d_db, hi - lo, 32, d_ans, d_fw, device=c.local, stream=c.stream)
         if ev:
             ev[1].record(c.stream)
 
@@ -727,7 +749,9 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
     gbs = fold_bytes / (f_ms * 1e-3) / 1e9
     return {"tree": {"kernel_ms": round(t_ms, 4), "aes_blocks_per_s": blocks / (t_ms * 1e-3),
                      "kernels": "k_unpack + k_evalfull"},
-            "fold": {"kernel_ms": round(f_ms, 4), "kernels": "k_fold* + k_xor_parts",
+            "fold": {"kernel_ms": round(f_ms, 4),
+                     "kernels": ("k_fold_mfma / k_fold_sliced_direct (bit-sliced DB)" if c.args.pir_fold == "mfma"
+                                 else "k_fold_direct / k_fold4r (row-major DB)") + " + k_xor_parts",
                      "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                                   "algorithmic_bytes": fold_bytes,
@@ -771,6 +795,7 @@ def wl_pir(c: Ctx) -> dict:
                                     profiled_shape=(W == 1 and nk == 64))
     line["roofline"]["step_kernel_ms"] = round(k_ms, 4)
     line["roofline"]["fold"] = kern["fold"]["roofline"]
+    line["pir_db"] = c.pir_layout
     if c.world == 1 and not a.no_sweep:
         # B in {1, 16, 64, 256}; the fold reads the DB once per
         # batch up to 256 keys (pir_kernels.hip plan_fold).
@@ -807,8 +832,9 @@ def sub_workloads(c: Ctx) -> dict:
                                 if k in ln["roofline"]}
             if "gate" in ln["roofline"]:
                 keep["roofline"]["gate_frac"] = ln["roofline"]["gate"]["frac"]
-            if "kernels" in ln:
-                keep["kernels"] = ln["kernels"]
+            for k in ("kernels", "pir_db"):
+                if k in ln:
+                    keep[k] = ln[k]
             out[name] = keep
     finally:
         vars(a).update(saved)
@@ -874,6 +900,8 @@ def main() -> None:
     ap.add_argument("--split-logN", type=int, default=32)
     ap.add_argument("--pir-logN", type=int, default=24)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--pir-fold", choices=["mfma", "lds"], default="mfma",
+                    help="pir: XOR fold on the matrix cores over the bit-sliced DB (default) or the LDS fold")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="split/pir on 1 GPU: time rank 0's share of a W-way split")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1096,6 +1096,7 @@ int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size
 struct PirDb {
     uint32_t logN = 0, pbits = 0;
     uint64_t nrec = 0;
+    bool sliced = true;            // shards in the bit-sliced layout (the matrix-core fold)
     DevList devs;                  // per shard: its device
     std::vector<void*> shard;      // per device: its DB slice
     std::vector<uint64_t> shard_n; // records in that slice
@@ -1123,19 +1124,37 @@ int dpf_pir_db_create(const uint8_t* db, uint64_t nrec, uint32_t logN, int ngpus
     h->logN = logN;
     h->pbits = pb;
     h->nrec = nrec;
+    // DPF_PIR_FOLD=lds keeps the row-major shards and the LDS fold (A/B runs).
+    static const bool lds = [] {
+        const char* e = getenv("DPF_PIR_FOLD");
+        return e && e[0] == 'l';
+    }();
+    h->sliced = !lds;
     const uint64_t slice = 1ull << (logN - pb);
     for (int g = 0; g < want; ++g) {
         const uint64_t lo = std::min<uint64_t>(nrec, (uint64_t)g * slice);
         const uint64_t hi = std::min<uint64_t>(nrec, lo + slice);
         DeviceGuard gd(devs[(size_t)g]->id);
         void* p = nullptr;
-        const size_t bytes = std::max<uint64_t>(hi - lo, 1) * 32;
+        const size_t bytes = h->sliced ? dpf_pir_db_sliced_size(hi - lo) : std::max<uint64_t>(hi - lo, 1) * 32;
         if (hipMalloc(&p, bytes) != hipSuccess) return fail(DPF_ERR_NOMEM, "dpf: DB shard allocation failed");
         h->devs.push_back(devs[(size_t)g]);     // ~PirDb frees what was allocated so far
         h->shard.push_back(p);
         h->shard_n.push_back(hi - lo);
-        if (hi > lo && hipMemcpy(p, db + lo * 32, (hi - lo) * 32, hipMemcpyHostToDevice) != hipSuccess)
-            return fail(DPF_ERR_HIP, "dpf: DB upload failed");
+        if (hi <= lo) continue;
+        if (!h->sliced) {
+            if (hipMemcpy(p, db + lo * 32, (hi - lo) * 32, hipMemcpyHostToDevice) != hipSuccess)
+                return fail(DPF_ERR_HIP, "dpf: DB upload failed");
+            continue;
+        }
+        // Row-major records up through a staging buffer, sliced once on the device.
+        void* tmp = nullptr;
+        if (hipMalloc(&tmp, (hi - lo) * 32) != hipSuccess) return fail(DPF_ERR_NOMEM, "dpf: DB staging allocation failed");
+        const bool ok = hipMemcpy(tmp, db + lo * 32, (hi - lo) * 32, hipMemcpyHostToDevice) == hipSuccess &&
+                        dpfk::launch_slice_db((const uint8_t*)tmp, hi - lo, (uint8_t*)p, nullptr) == hipSuccess &&
+                        hipDeviceSynchronize() == hipSuccess;
+        (void)hipFree(tmp);
+        if (!ok) return fail(DPF_ERR_HIP, "dpf: DB upload failed");
     }
     *handle = h.release();
     return DPF_OK;
@@ -1156,8 +1175,9 @@ int dpf_pir_answer(void* handle, const uint8_t* keys, size_t klen, size_t nkeys,
         HIP_TRY(hipError_t(d.work.ensure(dpf_pir_workspace_size(nkeys, h->logN, h->pbits))));
         HIP_TRY(hipError_t(d.out.ensure(std::max<size_t>(32, nkeys * 32))));
         HIP_TRY(hipMemcpyAsync(d.keys.p, keys, nkeys * klen, hipMemcpyHostToDevice, d.st));
-        int r = dpf_pir_answer_dev(d.id, (const uint8_t*)d.keys.p, klen, nkeys, h->logN, h->pbits, lo,
-                                   (const uint8_t*)h->shard[lo], h->shard_n[lo], (uint8_t*)d.out.p, d.work.p, d.st);
+        int r = (h->sliced ? dpf_pir_answer_sliced_dev : dpf_pir_answer_dev)(
+            d.id, (const uint8_t*)d.keys.p, klen, nkeys, h->logN, h->pbits, lo, (const uint8_t*)h->shard[lo],
+            h->shard_n[lo], (uint8_t*)d.out.p, d.work.p, d.st);
         if (r) return r;
         HIP_TRY(hipMemcpyAsync(part[lo].data(), d.out.p, nkeys * 32, hipMemcpyDeviceToHost, d.st));
         HIP_TRY(hipStreamSynchronize(d.st));

@@ -656,11 +656,12 @@ typedef int fold_v8i __attribute__((ext_vector_type(8)));
 typedef float fold_v16f __attribute__((ext_vector_type(16)));
 
 // Which side takes the cheap 5-op expansion (ANDs + one shift; weights 0.5,
-// 1, 2, 2) and which the 7-op one (weights 2, 1, 0.5, 0.5): the selection
-// side is expanded once per MT x NT tile group for NT tiles, the DB side for
-// MT, so the side shared by fewer MFMAs should be the cheap one.
+// 1, 2, 2) and which the 7-op one (weights 2, 1, 0.5, 0.5): a selection
+// operand feeds NT MFMAs and a DB operand MT, so per MFMA the VALU cost is
+// sel/NT + db/MT, lowest with the cheap form on the side with fewer tiles
+// (kernel template below; DPF_FOLD_SEL_CHEAP=0/1 forces one for A/B runs).
 #ifndef DPF_FOLD_SEL_CHEAP
-#define DPF_FOLD_SEL_CHEAP 1
+#define DPF_FOLD_SEL_CHEAP -1
 #endif
 __device__ __forceinline__ fold_v8i fp4_w5(uint32_t x) {     // weights 0.5, 1, 2, 2
     fold_v8i r;
@@ -680,8 +681,10 @@ __device__ __forceinline__ fold_v8i fp4_w7(uint32_t s) {     // weights 2, 1, 0.
     r[4] = r[5] = r[6] = r[7] = 0;
     return r;
 }
-__device__ __forceinline__ fold_v8i fp4_db(uint32_t x) { return DPF_FOLD_SEL_CHEAP ? fp4_w7(x) : fp4_w5(x); }
-__device__ __forceinline__ fold_v8i fp4_sel(uint32_t s) { return DPF_FOLD_SEL_CHEAP ? fp4_w5(s) : fp4_w7(s); }
+template <bool SC>
+__device__ __forceinline__ fold_v8i fp4_db(uint32_t x) { return SC ? fp4_w7(x) : fp4_w5(x); }
+template <bool SC>
+__device__ __forceinline__ fold_v8i fp4_sel(uint32_t s) { return SC ? fp4_w5(s) : fp4_w7(s); }
 __device__ __forceinline__ uint32_t u4w(const uint4& v, int t) { return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w; }
 
 constexpr int kFoldFp4 = 4;         // cbsz / blgp format code of e2m1
@@ -695,19 +698,24 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 // latency under load).  Loaded straight into the operand lanes, 16 B per
 // lane from 32 rows 2 MiB apart, the fold fetched ~1.6x its bytes and ran at
 // a third of the HBM rate (profiles/r04/fold_v1).
-template <int MT, int NT, int SG>
-__global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
+// KG key groups per workgroup: wave w takes bit slice w % (8/NT) of key
+// group w / (8/NT), so a workgroup covers 32*MT*KG keys x 256 bits.
+template <int MT, int NT, int SG, int KG>
+__global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words) {
-    constexpr int NW = 8 / NT;
-    constexpr int kRows = 32 * MT;
+    constexpr int NS = 8 / NT;                                 // bit slices
+    constexpr int NW = NS * KG;
+    constexpr bool SC = DPF_FOLD_SEL_CHEAP >= 0 ? DPF_FOLD_SEL_CHEAP == 1 : NT < MT;
+    constexpr int kRows = 32 * MT * KG;
     constexpr int kRow = SG * 8 + 4;                           // words per staged row (+4: conflict-free b128 reads)
     constexpr int kPieces = kRows * (SG * 2);                  // uint4 pieces per staged block
     constexpr int kPer = (kPieces + 64 * NW - 1) / (64 * NW);  // per thread
     __shared__ __attribute__((aligned(16))) uint32_t s_sel[kRows * kRow];
     zero_answers(zero, zero_words);
     const uint32_t l = threadIdx.x & 63, h = l >> 5, r = l & 31;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = wv % NS, kg = wv / NS;                   // bit slice, key group
     const uint64_t s0 = (uint64_t)blockIdx.x * sg_per_block;
     const uint64_t s1 = s0 + sg_per_block < nsg ? s0 + sg_per_block : nsg;
     if (s0 >= s1) return;                                       // uniform over the workgroup
@@ -752,15 +760,15 @@ __global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_
         uint4 A[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-            A[m] = *reinterpret_cast<const uint4*>(&s_sel[(32 * m + r) * kRow + 8 * sl + 4 * h]);
+            A[m] = *reinterpret_cast<const uint4*>(&s_sel[(32 * (MT * kg + m) + r) * kRow + 8 * sl + 4 * h]);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             fold_v8i bo[NT];
 #pragma unroll
-            for (int j = 0; j < NT; ++j) bo[j] = fp4_db(u4w(B[j], t));
+            for (int j = 0; j < NT; ++j) bo[j] = fp4_db<SC>(u4w(B[j], t));
 #pragma unroll
             for (int m = 0; m < MT; ++m) {
-                const fold_v8i ao = fp4_sel(u4w(A[m], t));
+                const fold_v8i ao = fp4_sel<SC>(u4w(A[m], t));
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
                     acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ao, bo[j], acc[m][j], kFoldFp4, kFoldFp4,
@@ -794,7 +802,7 @@ __global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_
     }
     if (sb < s1) block(sb, BA, BB);
     // Parities -> answer words: parts[block][key][8] (word = bit tile).
-    constexpr uint32_t pkeys = 32 * MT;
+    constexpr uint32_t pkeys = 32 * MT * KG;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -808,7 +816,7 @@ __global__ __launch_bounds__(64 * (8 / NT), (MT * NT <= 4) ? 2 : 1) void k_fold_
                 out = l == row0 ? (uint32_t)b : out;
                 out = l == row0 + 4 ? (uint32_t)(b >> 32) : out;
             }
-            if (l < 32) parts[((uint64_t)blockIdx.x * pkeys + 32 * m + l) * 8 + w * NT + j] = out;
+            if (l < 32) parts[((uint64_t)blockIdx.x * pkeys + 32 * (MT * kg + m) + l) * 8 + w * NT + j] = out;
         }
 }
 
@@ -842,6 +850,63 @@ __global__ __launch_bounds__(256) void k_slice_db(const uint4* __restrict__ db, 
     }
 }
 
+// Few keys over the sliced DB: no matrix product needed.  Thread n of a
+// 256-thread workgroup owns bit position n; per super-group it reads its 8
+// words dbs[S][n][0..7] (the workgroup: 8 KiB contiguous) and, for every key
+// k, XORs (selection word & DB word) into acc[k] -- one v_bitop3 per word and
+// key, the selection words wave-uniform (scalar loads).  The answer bit
+// (k, n) is the parity of popcount(acc[k]).  HBM-bound up to ~16 keys.
+template <int KB>
+__global__ __launch_bounds__(256) void k_fold_sliced_direct(const uint32_t* __restrict__ bits, uint64_t wpk,
+                                                            const uint4* __restrict__ dbs, uint64_t nsg,
+                                                            uint32_t nkeys, uint64_t sg_per_block,
+                                                            uint32_t* __restrict__ parts, uint32_t* __restrict__ zero,
+                                                            uint64_t zero_words) {
+    zero_answers(zero, zero_words);
+    const uint32_t n = threadIdx.x, l = n & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t s0 = (uint64_t)blockIdx.x * sg_per_block;
+    const uint64_t s1 = s0 + sg_per_block < nsg ? s0 + sg_per_block : nsg;
+    uint32_t acc[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) acc[k] = 0;
+    auto fold = [&](uint64_t S, const uint4& a, const uint4& b) __attribute__((always_inline)) {
+        const uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        const bool in = 8 * S + 8 <= wpk;                      // uniform
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            if ((uint32_t)k >= nkeys || !in) continue;         // uniform
+            const uint32_t* sel = bits + (uint64_t)k * wpk + 8 * S;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) acc[k] = xam(acc[k], x[g], sel[g]);
+        }
+        if (!in) {                                             // the key rows end inside this super-group
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                if ((uint32_t)k >= nkeys) continue;
+                const uint32_t* sel = bits + (uint64_t)k * wpk;
+#pragma unroll
+                for (int g = 0; g < 8; ++g)
+                    if (8 * S + g < wpk) acc[k] = xam(acc[k], x[g], sel[8 * S + g]);
+            }
+        }
+    };
+    uint64_t S = s0;
+    for (; S + 1 < s1; S += 2) {
+        const uint4 a0 = dbs[(S * 256 + n) * 2], b0 = dbs[(S * 256 + n) * 2 + 1];
+        const uint4 a1 = dbs[((S + 1) * 256 + n) * 2], b1 = dbs[((S + 1) * 256 + n) * 2 + 1];
+        fold(S, a0, b0);
+        fold(S + 1, a1, b1);
+    }
+    if (S < s1) fold(S, dbs[(S * 256 + n) * 2], dbs[(S * 256 + n) * 2 + 1]);
+    // parts[block][key][8]: wave w holds answer words 2w (lanes 0-31) and 2w+1.
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64((__builtin_popcount(acc[k]) & 1) != 0);
+        if (l < 2) parts[((uint64_t)blockIdx.x * KB + k) * 8 + 2 * w + l] = l ? (uint32_t)(m >> 32) : (uint32_t)m;
+    }
+}
+
 uint64_t pir_sliced_bytes(uint64_t nrec) { return (nrec + 255) / 256 * 256 * 32; }
 
 hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipStream_t st) {
@@ -854,32 +919,35 @@ hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipSt
 }
 
 namespace {
-template <int MT, int NT, int SG>
+template <int MT, int NT, int SG, int KG>
 hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
                           uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st) {
-    constexpr int NW = 8 / NT;
+    constexpr int NW = 8 / NT * KG;
     // Resident workgroups only (one round): each takes a contiguous run of
     // whole staged blocks.  (A fixed 4 workgroups per CU left 1/4 - 3/4 of
     // them for a second round at 3 or 1 resident per CU.)
     static int per_cu = [] {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_mfma<MT, NT, SG>, 64 * NW, 0) != hipSuccess || n < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_mfma<MT, NT, SG, KG>, 64 * NW, 0) != hipSuccess || n < 1)
             n = 1;
         return n;
     }();
     uint64_t spb;
     split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
-    hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+    hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
                        reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words);
     return hipGetLastError();
 }
 }  // namespace
 
-#ifndef DPF_FOLD_NT4
-#define DPF_FOLD_NT4 1   // bit tiles per wave at 65-128 keys (8 / NT waves per workgroup)
+// Tile shape per key count (32 keys per tile): MT key tiles x NT bit tiles
+// per wave, KG key groups per workgroup.  DPF_FOLD_SHAPE picks among
+// measured alternatives for 65-256 keys (A/B builds).
+#ifndef DPF_FOLD_SLICED_DIRECT
+#define DPF_FOLD_SLICED_DIRECT 16   // keys up to which the sliced fold uses k_fold_sliced_direct (0: MFMA always)
 #endif
-#ifndef DPF_FOLD_NT8
-#define DPF_FOLD_NT8 1   // ... at 129-256 keys
+#ifndef DPF_FOLD_SHAPE
+#define DPF_FOLD_SHAPE 0
 #endif
 hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
                                   uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
@@ -887,6 +955,28 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
     if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * 32, st);
     if (words_per_key % 4 != 0 || words_per_key * 32 < nrec) return hipErrorInvalidValue;
     const uint64_t nsg = (nrec + 255) / 256;
+    if (nkeys <= (uint32_t)DPF_FOLD_SLICED_DIRECT) {           // few keys: popcount fold, no MFMA
+        uint64_t blocks, spb;
+        split_chunks(nsg, (uint64_t)cu_count_fold() * 8, 2, blocks, spb);
+        const uint32_t kb = nkeys <= 1 ? 1 : nkeys <= 4 ? 4 : 16;
+        const uint4* d4 = reinterpret_cast<const uint4*>(dbs);
+        const dim3 g((uint32_t)blocks), bl(256);
+        if (kb == 1) {
+            hipLaunchKernelGGL(k_fold_sliced_direct<1>, g, bl, 0, st, bits, words_per_key, d4, nsg, nkeys, spb, parts, ans,
+                               (uint64_t)nkeys * 8);
+        } else if (kb == 4) {
+            hipLaunchKernelGGL(k_fold_sliced_direct<4>, g, bl, 0, st, bits, words_per_key, d4, nsg, nkeys, spb, parts, ans,
+                               (uint64_t)nkeys * 8);
+        } else {
+            hipLaunchKernelGGL(k_fold_sliced_direct<16>, g, bl, 0, st, bits, words_per_key, d4, nsg, nkeys, spb, parts,
+                               ans, (uint64_t)nkeys * 8);
+        }
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
+        hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nkeys, kb, 8u,
+                           ans, (uint64_t)8, 0u);
+        return hipGetLastError();
+    }
     for (uint32_t k0 = 0; k0 < nkeys; k0 += 256) {
         const uint32_t nk = nkeys - k0 < 256 ? nkeys - k0 : 256;
         const uint32_t* b = bits + (uint64_t)k0 * words_per_key;
@@ -895,10 +985,19 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
         uint64_t blocks = 0;
         uint32_t mt;
         hipError_t e;
-        if (nk <= 32) e = launch_mfma_mt<1, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 1;
-        else if (nk <= 64) e = launch_mfma_mt<2, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 2;
-        else if (nk <= 128) e = launch_mfma_mt<4, DPF_FOLD_NT4, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 4;
-        else e = launch_mfma_mt<8, DPF_FOLD_NT8, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 8;
+        if (nk <= 32) e = launch_mfma_mt<1, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 1;
+        else if (nk <= 64) e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 2;
+        else if (nk <= 128) {
+            mt = 4;
+            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            else e = launch_mfma_mt<4, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+        } else {
+            mt = 8;
+            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            else if (DPF_FOLD_SHAPE == 2) e = launch_mfma_mt<4, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            else if (DPF_FOLD_SHAPE == 3) e = launch_mfma_mt<2, 8, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            else e = launch_mfma_mt<8, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+        }
         if (e != hipSuccess) return e;
         const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
         hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk, 32 * mt,

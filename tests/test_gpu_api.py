@@ -84,11 +84,14 @@ def test_expanded_form_builds_byte_sliced_records_on_first_use():
 
 
 def test_workspace_reexpanded_by_another_entry_point_is_not_stale():
-    """a workspace registered with byte-sliced planes, then
-    re-expanded with OTHER keys by dpf_evalfull_subtree_dev under the T-table
-    back end, must not be evaluated from the old planes when the caller
-    switches back to byte-sliced: the registry follows every expansion.
-    dpf_forget_workspace drops the record (the next expanded call refuses)."""
+    """a workspace registered with byte-sliced planes, then used
+    for OTHER keys by dpf_evalfull_subtree_dev under the T-table back end,
+    must not be evaluated from the old planes when the caller switches back
+    to byte-sliced: the registry follows every entry point.  When the
+    one-shot call reads the key bytes directly (no expansion into d_work), the
+    record is dropped and the expanded call refuses; when it expands, the
+    planes are rebuilt from the new keys.  dpf_forget_workspace drops the
+    record (the next expanded call refuses)."""
     import torch
     logN, nk = 16, 8
     kl, olen = dpf.key_len(logN), dpf.evalfull_len(logN)
@@ -108,9 +111,14 @@ def test_workspace_reexpanded_by_another_entry_point_is_not_stale():
         dpf.evalfull_subtree_dev(d_b, kl, nk, logN, 0, 0, d_out, d_work)   # records of keys B only
         dpf.set_aes_impl("bitsliced")
         d_out.zero_()
-        dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)        # must rebuild planes from B
-        torch.cuda.synchronize()
-        assert np.array_equal(d_out.cpu().numpy().reshape(nk, olen), oracle.evalfull_batch(kb, logN, nthreads=4))
+        try:
+            dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)    # planes rebuilt from B, or refused
+        except dpf.DPFPanic as e:
+            assert e.code == dpf.DPF_ERR_PARAM                      # d_work no longer holds expanded keys
+        else:
+            torch.cuda.synchronize()
+            assert np.array_equal(d_out.cpu().numpy().reshape(nk, olen), oracle.evalfull_batch(kb, logN, nthreads=4))
+        dpf.expand_keys_dev(d_b, kl, nk, logN, d_work)
         dpf.forget_workspace(d_work)
         with pytest.raises(dpf.DPFPanic) as e:
             dpf.evalfull_expanded_dev(d_work, nk, logN, d_out)

@@ -190,3 +190,59 @@ def test_gather_xor_rccl_branch_and_eight_row_device_xor():
         assert np.array_equal(ans, rows[3])
     finally:
         dist.destroy_process_group()
+
+
+def test_in_library_multi_device_paths_on_eight_logical_devices():
+    """The library's own multi-device code (dpf_evalfull_split / _batch /
+    dpf_eval_batch over ngpus devices on one host thread each, the PIR handle
+    sharded by top-level subtree with the host XOR of the partials) has only
+    ever had one device to shard over.  dpf_gpu_init_devices([0] * 8) opens
+    the one GPU as 8 logical devices (each its own stream, mutex and
+    buffers), so every shard offset, thread and partial XOR of the 8-way paths
+    runs here against the oracle.  In a subprocess: the device registry is
+    process-wide."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import sys; sys.path[:0] = [%r, %r]
+import numpy as np, dpf, oracle
+from dpf import synth
+assert dpf.gpu_init_devices([0] * 8) == 8 and dpf.gpu_count() == 8
+dpf.set_small_call_path("gpu")
+logN = 24
+al, s0, s1 = synth.key_seeds(2, logN, first=31)
+ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+for n in (2, 4, 8):
+    out = dpf.evalfull_split(ka[0].tobytes(), logN, n)
+    x = out ^ dpf.evalfull_split(kb[0].tobytes(), logN, n)
+    bits = np.unpackbits(x, bitorder="little")
+    assert bits.sum() == 1 and bits[int(al[0])] == 1, n
+full = dpf.evalfull_split(ka[0].tobytes(), logN, 1)
+assert np.array_equal(out, full)
+for q in (0, 5, (1 << logN) - 1, int(al[0])):
+    assert ((int(out[q >> 3]) >> (q & 7)) & 1) == oracle.eval_(ka[0].tobytes(), q, logN, aesni=True)
+l2 = 14
+a2, t0, t1 = synth.key_seeds(37, l2, first=41)
+k2, _ = dpf.gen_batch_seeded(a2, l2, t0, t1)
+assert np.array_equal(dpf.evalfull_batch(k2, l2, ngpus=8), oracle.evalfull_batch(k2, l2, nthreads=8))
+xs = synth.eval_points(37, 50, l2)
+assert np.array_equal(dpf.eval_batch(k2, xs, l2, ngpus=8), oracle.eval_batch(k2, xs, l2, nthreads=8))
+lp = 16
+nrec = (1 << lp) - 1000
+db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+a3, u0, u1 = synth.key_seeds(9, lp, first=51)
+qa, qb = dpf.gen_batch_seeded(a3, lp, u0, u1)
+pdb = dpf.PirDB(db, lp, ngpus=8)
+ga, gb = pdb.answer(qa), pdb.answer(qb)
+pdb.close()
+for i in range(9):
+    assert ga[i].tobytes() == oracle.pir_answer(qa[i].tobytes(), lp, db, 0, nrec)
+    want = db[int(a3[i])] if a3[i] < nrec else np.zeros(32, np.uint8)
+    assert np.array_equal(ga[i] ^ gb[i], want)
+dpf.gpu_shutdown()
+print("done")
+''' % (os.path.join(root, "dpf-go_amd"), os.path.join(root, "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.strip().endswith("done")

@@ -7,7 +7,7 @@ cd "$REPO"
 OUT="gpurun_out/$1"; shift
 mkdir -p "$OUT"
 for r in 1 2; do
-  for b in 64 128 256; do
+  for b in ${FOLD_BS:-64 128 256}; do
     for v in "$@"; do
       FOLD_MODE=mfma timeout -k 10 120 tools/bin_fold_$v $b 32 24 > "$OUT/tmp.json" 2>> "$OUT/err.log"
       rc=$?; [ $rc -le 1 ] || { echo "$v $b rc=$rc"; exit $rc; }
