@@ -46,9 +46,6 @@
 #ifndef DPF_WALK_BATCH
 #define DPF_WALK_BATCH 1   // tree kernels' root-to-subtree walks: batched single-block rounds
 #endif
-#ifndef DPF_WALK_PREFETCH
-#define DPF_WALK_PREFETCH 1   // key records requested ahead of use in the tree kernels' prologue and walks
-#endif
 
 namespace dpfk {
 
@@ -447,19 +444,12 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     const uint64_t t_start = wall_clock64();
 #endif
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kTreeBlock
-#if !DPF_WALK_PREFETCH
     fill_table(s_tab);
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kTreeBlock
     if (u >= nunits) return;
-#endif
-    // DPF_WALK_PREFETCH: the key's root, final CW and first walk record are
-    // requested before the table fill (their latency overlaps it; the tail
-    // threads past nunits use the last unit's key and leave after the fill),
-    // and every walk step requests the next level's record before its AES.
-    const uint64_t uu = u < nunits ? u : nunits - 1;
-    uint64_t key = uu >> units_log;
+    uint64_t key = u >> units_log;
     if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
-    const uint64_t local = uu & ((1ull << units_log) - 1);
+    const uint64_t local = u & ((1ull << units_log) - 1);
     const uint64_t sub = sub_base + local;
     Ctx c;
     if constexpr (RAW) {
@@ -484,11 +474,6 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     Node n;
     n.s = key_root<RAW>(c.ks, n.t);
     uint32_t lvl = 0;
-#if DPF_WALK_PREFETCH
-    CW cw0 = key_cw<RAW>(c.ks, 0);                          // level 0's record (clamped use below)
-    fill_table(s_tab);
-    if (u >= nunits) return;
-#endif
     if constexpr (UNIFORM) {
         // Shared walk: when the whole workgroup (B = 2^W threads) evaluates
         // consecutive subtrees of one key, its threads' paths agree on the
@@ -505,19 +490,10 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
             if (threadIdx.x < 64) {
                 const uint64_t subj = (sub - threadIdx.x) + ((uint64_t)threadIdx.x << (W - 6));
                 Node m = n;
-#if DPF_WALK_PREFETCH
-                CW cw = cw0;
-                for (uint32_t i = 0; i < l1; ++i) {
-                    const CW nx = key_cw<RAW>(c.ks, i + 1 < l1 ? i + 1 : i);
-                    walk_step<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
-                    cw = nx;
-                }
-#else
                 for (uint32_t i = 0; i < l1; ++i) {
                     CW cw = key_cw<RAW>(c.ks, i);
                     walk_step<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
                 }
-#endif
                 uint32_t* f = s_front + 5 * threadIdx.x;
                 f[0] = m.s.c0; f[1] = m.s.c1; f[2] = m.s.c2; f[3] = m.s.c3; f[4] = m.t;
             }
@@ -528,21 +504,10 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
             lvl = l1;
         }
     }
-#if DPF_WALK_PREFETCH
-    if (lvl < ltop) {
-        CW cw = lvl == 0 ? cw0 : key_cw<RAW>(c.ks, lvl);
-        for (uint32_t i = lvl; i < ltop; ++i) {
-            const CW nx = key_cw<RAW>(c.ks, i + 1 < ltop ? i + 1 : i);
-            walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
-            cw = nx;
-        }
-    }
-#else
     for (uint32_t i = lvl; i < ltop; ++i) {
         CW cw = key_cw<RAW>(c.ks, i);
         walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
-#endif
     // Lane pairs share a key when a wave owns one key (UNIFORM): whole-line
     // leaf stores (dfs PAIR).  DPF_PAIR_STORES=0 builds the r02 half-line
     // stores for A/B runs.

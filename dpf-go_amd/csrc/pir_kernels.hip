@@ -855,7 +855,10 @@ __global__ __launch_bounds__(256) void k_slice_db(const uint4* __restrict__ db, 
 // words dbs[S][n][0..7] (the workgroup: 8 KiB contiguous) and, for every key
 // k, XORs (selection word & DB word) into acc[k] -- one v_bitop3 per word and
 // key, the selection words wave-uniform (scalar loads).  The answer bit
-// (k, n) is the parity of popcount(acc[k]).  HBM-bound up to ~16 keys.
+// (k, n) is the parity of popcount(acc[k]).  Used for one key (97 us at
+// configs[4] against the MFMA fold's 103): with 4 or 16 keys its per-key
+// scalar loads serialise (131 / 388 us against 104 / 107,
+// profiles/r04/fold_ab/).
 template <int KB>
 __global__ __launch_bounds__(256) void k_fold_sliced_direct(const uint32_t* __restrict__ bits, uint64_t wpk,
                                                             const uint4* __restrict__ dbs, uint64_t nsg,
@@ -944,7 +947,7 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
 // per wave, KG key groups per workgroup.  DPF_FOLD_SHAPE picks among
 // measured alternatives for 65-256 keys (A/B builds).
 #ifndef DPF_FOLD_SLICED_DIRECT
-#define DPF_FOLD_SLICED_DIRECT 16   // keys up to which the sliced fold uses k_fold_sliced_direct (0: MFMA always)
+#define DPF_FOLD_SLICED_DIRECT 1    // keys up to which the sliced fold uses k_fold_sliced_direct (0: MFMA always)
 #endif
 #ifndef DPF_FOLD_SHAPE
 #define DPF_FOLD_SHAPE 0
@@ -955,22 +958,12 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
     if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * 32, st);
     if (words_per_key % 4 != 0 || words_per_key * 32 < nrec) return hipErrorInvalidValue;
     const uint64_t nsg = (nrec + 255) / 256;
-    if (nkeys <= (uint32_t)DPF_FOLD_SLICED_DIRECT) {           // few keys: popcount fold, no MFMA
+    if (nkeys <= (uint32_t)DPF_FOLD_SLICED_DIRECT) {           // one key: popcount fold, no MFMA
         uint64_t blocks, spb;
         split_chunks(nsg, (uint64_t)cu_count_fold() * 8, 2, blocks, spb);
-        const uint32_t kb = nkeys <= 1 ? 1 : nkeys <= 4 ? 4 : 16;
-        const uint4* d4 = reinterpret_cast<const uint4*>(dbs);
-        const dim3 g((uint32_t)blocks), bl(256);
-        if (kb == 1) {
-            hipLaunchKernelGGL(k_fold_sliced_direct<1>, g, bl, 0, st, bits, words_per_key, d4, nsg, nkeys, spb, parts, ans,
-                               (uint64_t)nkeys * 8);
-        } else if (kb == 4) {
-            hipLaunchKernelGGL(k_fold_sliced_direct<4>, g, bl, 0, st, bits, words_per_key, d4, nsg, nkeys, spb, parts, ans,
-                               (uint64_t)nkeys * 8);
-        } else {
-            hipLaunchKernelGGL(k_fold_sliced_direct<16>, g, bl, 0, st, bits, words_per_key, d4, nsg, nkeys, spb, parts,
-                               ans, (uint64_t)nkeys * 8);
-        }
+        const uint32_t kb = 1;
+        hipLaunchKernelGGL(k_fold_sliced_direct<1>, dim3((uint32_t)blocks), dim3(256), 0, st, bits, words_per_key,
+                           reinterpret_cast<const uint4*>(dbs), nsg, nkeys, spb, parts, ans, (uint64_t)nkeys * 8);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
         const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
         hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nkeys, kb, 8u,
