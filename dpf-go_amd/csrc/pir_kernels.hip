@@ -952,6 +952,9 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
 #ifndef DPF_FOLD_SHAPE
 #define DPF_FOLD_SHAPE 0
 #endif
+#ifndef DPF_FOLD_SHAPE64
+#define DPF_FOLD_SHAPE64 0   // 33-64 keys
+#endif
 hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
                                   uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
     if (nkeys == 0) return hipSuccess;
@@ -979,7 +982,13 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
         uint32_t mt;
         hipError_t e;
         if (nk <= 32) e = launch_mfma_mt<1, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 1;
-        else if (nk <= 64) e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 2;
+        else if (nk <= 64) {
+            mt = 2;
+            if (DPF_FOLD_SHAPE64 == 1) e = launch_mfma_mt<2, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            else if (DPF_FOLD_SHAPE64 == 2) e = launch_mfma_mt<1, 2, 4, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            else if (DPF_FOLD_SHAPE64 == 3) e = launch_mfma_mt<2, 4, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            else e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+        }
         else if (nk <= 128) {
             mt = 4;
             if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
