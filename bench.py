@@ -120,7 +120,7 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
         r["traffic_note"] = "no PMC profile at this per-rank shape (1/N of the 1-GPU split); traffic not reported"
         return r
     if workload != "evalfull":
-        for rnd in ("r03", "r02"):
+        for rnd in ("r04", "r03", "r02"):
             name = f"{rnd}_traffic_{workload}.json"
             try:
                 with open(os.path.join(ROOT, "profiles", name)) as f:
@@ -135,7 +135,7 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
             r["traffic_source"] = f"profiles/{name} (sum of {', '.join(ks)})"
             break
         return r
-    for name in ("r03_traffic.json", "r02_traffic.json", "r01_traffic.json"):
+    for name in ("r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01_traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 t = json.load(f)
@@ -747,13 +747,31 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
     blocks = nk * (3 * (1 << (stop_of(logN) - pb)) - 2)
     fold_bytes = (hi - lo) * 32 + nk * per_key          # DB slice + selection bits, read once
     gbs = fold_bytes / (f_ms * 1e-3) / 1e9
+    # Measured HBM bytes of the fold kernels from the committed PMC passes of
+    # this exact shape (1 GPU, 64 keys, the fold this run uses).
+    traffic, tsrc = None, None
+    if W == 1 and nk == 64:
+        for rnd in ("r04", "r03"):
+            name = f"{rnd}_traffic_pir.json"
+            try:
+                with open(os.path.join(ROOT, "profiles", name)) as f:
+                    t = json.load(f)
+            except Exception:
+                continue
+            want = ("k_fold_mfma", "k_fold_sliced") if c.args.pir_fold == "mfma" else ("k_fold4r", "k_fold_direct")
+            ks = [k for k in t if k.startswith(want + ("k_xor_parts",))]
+            if any(k.startswith(want) for k in ks):
+                traffic, tsrc = round(sum(t[k]["traffic_bytes"] for k in ks)), f"profiles/{name} ({', '.join(sorted(ks))})"
+                break
     return {"tree": {"kernel_ms": round(t_ms, 4), "aes_blocks_per_s": blocks / (t_ms * 1e-3),
                      "kernels": "k_unpack + k_evalfull"},
             "fold": {"kernel_ms": round(f_ms, 4),
                      "kernels": ("k_fold_mfma / k_fold_sliced_direct (bit-sliced DB)" if c.args.pir_fold == "mfma"
                                  else "k_fold_direct / k_fold4r (row-major DB)") + " + k_xor_parts",
                      "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                                  **({"traffic_source": tsrc,
+                                      "traffic_over_algorithmic": round(traffic / fold_bytes, 3)} if traffic else {}),
                                   "algorithmic_bytes": fold_bytes,
                                   "note": "DB slice + selection bits read once per batch; the measured streaming-read "
                                           "ceiling of this chip is ~6.17 TB/s (tools/hbm_read.hip)"}}}
