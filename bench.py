@@ -744,6 +744,18 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
 
     _, t_ms = c.timed(tree, steps, 3)
     _, f_ms = c.timed(fold, steps, 3)
+    # The same two phases back to back, as in a step, with an event between
+    # them: each phase's time when it follows the other.
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in evs:
+        e[0].record(c.stream)
+        tree(None)
+        e[1].record(c.stream)
+        fold(None)
+        e[2].record(c.stream)
+    torch.cuda.synchronize(c.dev)
+    in_step = {"tree_ms": round(sum(e[0].elapsed_time(e[1]) for e in evs) / steps, 4),
+               "fold_ms": round(sum(e[1].elapsed_time(e[2]) for e in evs) / steps, 4)}
     blocks = nk * (3 * (1 << (stop_of(logN) - pb)) - 2)
     fold_bytes = (hi - lo) * 32 + nk * per_key          # DB slice + selection bits, read once
     gbs = fold_bytes / (f_ms * 1e-3) / 1e9
@@ -763,7 +775,8 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
             if any(k.startswith(want) for k in ks):
                 traffic, tsrc = round(sum(t[k]["traffic_bytes"] for k in ks)), f"profiles/{name} ({', '.join(sorted(ks))})"
                 break
-    return {"tree": {"kernel_ms": round(t_ms, 4), "aes_blocks_per_s": blocks / (t_ms * 1e-3),
+    return {"back_to_back": in_step,
+            "tree": {"kernel_ms": round(t_ms, 4), "aes_blocks_per_s": blocks / (t_ms * 1e-3),
                      "kernels": "k_unpack + k_evalfull"},
             "fold": {"kernel_ms": round(f_ms, 4),
                      "kernels": ("k_fold_mfma / k_fold_sliced_direct (bit-sliced DB)" if c.args.pir_fold == "mfma"

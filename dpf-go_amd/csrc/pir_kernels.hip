@@ -698,6 +698,9 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 // latency under load).  Loaded straight into the operand lanes, 16 B per
 // lane from 32 rows 2 MiB apart, the fold fetched ~1.6x its bytes and ran at
 // a third of the HBM rate (profiles/r04/fold_v1).
+#ifndef DPF_FOLD_PD
+#define DPF_FOLD_PD 1   // staged blocks in flight ahead of the one being folded (1 or 2)
+#endif
 // KG key groups per workgroup: wave w takes bit slice w % (8/NT) of key
 // group w / (8/NT), so a workgroup covers 32*MT*KG keys x 256 bits.
 template <int MT, int NT, int SG, int KG>
@@ -776,6 +779,38 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
             }
         }
     };
+#if DPF_FOLD_PD >= 2
+    // Two blocks in flight: block i folds from buffer i%3 while blocks i+1
+    // and i+2 load (selection words and DB pieces rotate over 3 sets).
+    uint4 sv0[kPer], sv1[kPer], sv2[kPer];
+    uint4 B0[SG][NT], B1[SG][NT], B2[SG][NT];
+    load_sel(s0, sv0);
+    load_db(s0, B0);
+    load_sel(s0 + SG < s1 ? s0 + SG : s0, sv1);
+    load_db(s0 + SG < s1 ? s0 + SG : s0, B1);
+    auto block = [&](uint64_t sb, const uint4 (&Bc)[SG][NT], uint4 (&Bf)[SG][NT], const uint4 (&svc)[kPer],
+                     uint4 (&svf)[kPer]) __attribute__((always_inline)) {
+        fold_prio(sb - s0, s1 - s0);
+        __syncthreads();                                        // previous block's operand reads are done
+        store_sel(svc);
+        __syncthreads();
+        const uint64_t nb = sb + 2 * SG < s1 ? sb + 2 * SG : sb;   // block after next (clamped)
+        load_sel(nb, svf);
+        load_db(nb, Bf);
+        const uint64_t n = s1 - sb;
+#pragma unroll
+        for (int sl = 0; sl < SG; ++sl)
+            if ((uint64_t)sl < n) fold_sg(sl, Bc[sl]);
+    };
+    uint64_t sb = s0;
+    for (; sb + 2 * SG < s1; sb += 3 * SG) {
+        block(sb, B0, B2, sv0, sv2);
+        block(sb + SG, B1, B0, sv1, sv0);
+        block(sb + 2 * SG, B2, B1, sv2, sv1);
+    }
+    if (sb < s1) block(sb, B0, B2, sv0, sv2);
+    if (sb + SG < s1) block(sb + SG, B1, B0, sv1, sv0);
+#else
     uint4 sv[kPer];
     uint4 BA[SG][NT], BB[SG][NT];
     load_sel(s0, sv);
@@ -801,6 +836,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
         block(sb + SG, BB, BA);
     }
     if (sb < s1) block(sb, BA, BB);
+#endif
     // Parities -> answer words: parts[block][key][8] (word = bit tile).
     constexpr uint32_t pkeys = 32 * MT * KG;
 #pragma unroll
