@@ -127,8 +127,10 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
                     t = json.load(f)
             except Exception:
                 continue
-            # PIR: the roofline is the tree's (k_unpack + k_evalfull); the fold has its own.
-            ks = sorted(k for k in t if k.startswith("k_") and (workload != "pir" or not k.startswith(("k_fold", "k_xor"))))
+            # PIR: the roofline is the tree's (k_unpack + k_evalfull); the fold has its
+            # own, and k_slice_db runs once per DB load, not per step.
+            ks = sorted(k for k in t if k.startswith("k_") and not k.startswith("k_slice")
+                        and (workload != "pir" or not k.startswith(("k_fold", "k_xor"))))
             tot = sum(t[k]["traffic_bytes"] for k in ks)
             r["traffic"] = round(tot)
             r["traffic_over_algorithmic"] = round(tot / hbm_bytes, 3)
@@ -141,10 +143,12 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
                 t = json.load(f)
         except Exception:
             continue
-        if kernel in t:
-            r["traffic"] = round(t[kernel]["traffic_bytes"])
-            r["traffic_over_algorithmic"] = round(t[kernel]["traffic_bytes"] / hbm_bytes, 3)
-            r["traffic_source"] = f"profiles/{name}"
+        # r04 kernel names carry the raw-key flag: k_evalfull<7, true, false, true>.
+        hit = kernel if kernel in t else next((k for k in t if k.startswith(kernel.rstrip(">"))), None)
+        if hit:
+            r["traffic"] = round(t[hit]["traffic_bytes"])
+            r["traffic_over_algorithmic"] = round(t[hit]["traffic_bytes"] / hbm_bytes, 3)
+            r["traffic_source"] = f"profiles/{name} ({hit})"
             break
     return r
 

@@ -703,10 +703,14 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 #endif
 // KG key groups per workgroup: wave w takes bit slice w % (8/NT) of key
 // group w / (8/NT), so a workgroup covers 32*MT*KG keys x 256 bits.
-template <int MT, int NT, int SG, int KG>
+// SGM: the selection bits are super-group-major, sel[S][sgm_keys][8 words]
+// (a staged block is then one contiguous read per super-group) instead of
+// EvalFull's key-major [key][wpk words].
+template <int MT, int NT, int SG, int KG, bool SGM = false>
 __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
-    uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words) {
+    uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
+    uint32_t sgm_keys = 0) {
     constexpr int NS = 8 / NT;                                 // bit slices
     constexpr int NW = NS * KG;
     constexpr bool SC = DPF_FOLD_SEL_CHEAP >= 0 ? DPF_FOLD_SEL_CHEAP == 1 : NT < MT;
@@ -723,14 +727,27 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
     const uint64_t s1 = s0 + sg_per_block < nsg ? s0 + sg_per_block : nsg;
     if (s0 >= s1) return;                                       // uniform over the workgroup
     // Staging role: piece p = threadIdx.x + i*64*NW is row p/(2SG), 16 bytes p%(2SG).
+    // Piece p -> (row, q = 16-byte piece of the row's block span): key-major,
+    // row = p / 2SG; super-group-major, p = (s * kRows + row) * 2 + half.
+    auto piece = [&](uint32_t p, uint32_t& row, uint32_t& q) __attribute__((always_inline)) {
+        if constexpr (SGM) {
+            row = (p >> 1) % kRows;
+            q = 2 * ((p >> 1) / kRows) + (p & 1);
+        } else {
+            row = p / (2 * SG);
+            q = p % (2 * SG);
+        }
+    };
     auto load_sel = [&](uint64_t sb, uint4 (&v)[kPer]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const uint32_t p = threadIdx.x + (uint32_t)i * 64 * NW;
-            const uint32_t row = p / (2 * SG), q = p % (2 * SG);
+            uint32_t row, q;
+            piece(p, row, q);
             const uint64_t word = sb * 8 + 4 * q;
             const bool ok = p < (uint32_t)kPieces && row < nkeys && word + 4 <= wpk;
-            const uint4 x = *reinterpret_cast<const uint4*>(bits + (uint64_t)(ok ? row : 0) * wpk + (ok ? word : 0));
+            const uint64_t at = SGM ? ((sb + q / 2) * sgm_keys + row) * 8 + 4 * (q & 1) : (uint64_t)row * wpk + word;
+            const uint4 x = *reinterpret_cast<const uint4*>(bits + (ok ? at : 0));
             v[i] = ok ? x : make_uint4(0, 0, 0, 0);
         }
     };
@@ -738,8 +755,9 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const uint32_t p = threadIdx.x + (uint32_t)i * 64 * NW;
-            if (p < (uint32_t)kPieces)
-                *reinterpret_cast<uint4*>(&s_sel[(p / (2 * SG)) * kRow + 4 * (p % (2 * SG))]) = v[i];
+            uint32_t row, q;
+            piece(p, row, q);
+            if (p < (uint32_t)kPieces) *reinterpret_cast<uint4*>(&s_sel[row * kRow + 4 * q]) = v[i];
         }
     };
     // DB pieces of a whole block (clamped past the range; never folded).
@@ -960,7 +978,8 @@ hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipSt
 namespace {
 template <int MT, int NT, int SG, int KG>
 hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
-                          uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st) {
+                          uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st,
+                          uint32_t sgm_keys = 0) {
     constexpr int NW = 8 / NT * KG;
     // Resident workgroups only (one round): each takes a contiguous run of
     // whole staged blocks.  (A fixed 4 workgroups per CU left 1/4 - 3/4 of
@@ -973,8 +992,12 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
     }();
     uint64_t spb;
     split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
-    hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                       reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words);
+    if (sgm_keys)
+        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, true>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, sgm_keys);
+    else
+        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words);
     return hipGetLastError();
 }
 }  // namespace
@@ -992,12 +1015,12 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
 #define DPF_FOLD_SHAPE64 0   // 33-64 keys
 #endif
 hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
-                                  uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st) {
+                                  uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st, uint32_t sgm_keys) {
     if (nkeys == 0) return hipSuccess;
     if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * 32, st);
     if (words_per_key % 4 != 0 || words_per_key * 32 < nrec) return hipErrorInvalidValue;
     const uint64_t nsg = (nrec + 255) / 256;
-    if (nkeys <= (uint32_t)DPF_FOLD_SLICED_DIRECT) {           // one key: popcount fold, no MFMA
+    if (nkeys <= (uint32_t)DPF_FOLD_SLICED_DIRECT && !sgm_keys) {   // one key: popcount fold, no MFMA
         uint64_t blocks, spb;
         split_chunks(nsg, (uint64_t)cu_count_fold() * 8, 2, blocks, spb);
         const uint32_t kb = 1;
@@ -1011,30 +1034,30 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
     }
     for (uint32_t k0 = 0; k0 < nkeys; k0 += 256) {
         const uint32_t nk = nkeys - k0 < 256 ? nkeys - k0 : 256;
-        const uint32_t* b = bits + (uint64_t)k0 * words_per_key;
+        const uint32_t* b = bits + (sgm_keys ? (uint64_t)k0 * 8 : (uint64_t)k0 * words_per_key);
         uint32_t* zero = k0 == 0 ? ans : nullptr;
         const uint64_t zw = k0 == 0 ? (uint64_t)nkeys * 8 : 0;
         uint64_t blocks = 0;
         uint32_t mt;
         hipError_t e;
-        if (nk <= 32) e = launch_mfma_mt<1, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st), mt = 1;
+        if (nk <= 32) e = launch_mfma_mt<1, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys), mt = 1;
         else if (nk <= 64) {
             mt = 2;
-            if (DPF_FOLD_SHAPE64 == 1) e = launch_mfma_mt<2, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
-            else if (DPF_FOLD_SHAPE64 == 2) e = launch_mfma_mt<1, 2, 4, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
-            else if (DPF_FOLD_SHAPE64 == 3) e = launch_mfma_mt<2, 4, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
-            else e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            if (DPF_FOLD_SHAPE64 == 1) e = launch_mfma_mt<2, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            else if (DPF_FOLD_SHAPE64 == 2) e = launch_mfma_mt<1, 2, 4, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            else if (DPF_FOLD_SHAPE64 == 3) e = launch_mfma_mt<2, 4, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            else e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
         }
         else if (nk <= 128) {
             mt = 4;
-            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
-            else e = launch_mfma_mt<4, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            else e = launch_mfma_mt<4, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
         } else {
             mt = 8;
-            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
-            else if (DPF_FOLD_SHAPE == 2) e = launch_mfma_mt<4, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
-            else if (DPF_FOLD_SHAPE == 3) e = launch_mfma_mt<2, 8, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
-            else e = launch_mfma_mt<8, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st);
+            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            else if (DPF_FOLD_SHAPE == 2) e = launch_mfma_mt<4, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            else if (DPF_FOLD_SHAPE == 3) e = launch_mfma_mt<2, 8, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            else e = launch_mfma_mt<8, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
         }
         if (e != hipSuccess) return e;
         const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);

@@ -58,9 +58,26 @@ int main(int argc, char** argv) {
                                  (uint32_t*)ans, (uint32_t*)parts, 0));
         CK(hipMemcpy(ref.data(), ans, ref.size(), hipMemcpyDeviceToHost));
     }
+    // FOLD_SGM=1 (with FOLD_MODE=mfma): the selection bits super-group-major,
+    // sgm[S][key][8 words] = bits[key][8S .. 8S+8), as a tree pass could write them.
+    const bool sgm = mfma && getenv("FOLD_SGM") && getenv("FOLD_SGM")[0] == '1';
+    void* bits_sgm = nullptr;
+    if (sgm) {
+        const uint64_t nsgs = (nrec + 255) / 256;
+        std::vector<uint32_t> t(nsgs * nkeys * 8, 0);
+        for (uint64_t S = 0; S < nsgs; ++S)
+            for (uint32_t k = 0; k < nkeys; ++k)
+                for (int w = 0; w < 8; ++w)
+                    if (8 * S + w < wpk) t[(S * nkeys + k) * 8 + w] = h[(size_t)k * wpk + 8 * S + w];
+        CK(hipMalloc(&bits_sgm, t.size() * 4));
+        CK(hipMemcpy(bits_sgm, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    }
     auto run = [&]() {
         CK(hipMemsetAsync(ans, 0, (size_t)nkeys * rec_bytes, 0));
-        if (mfma)
+        if (sgm)
+            CK(dpfk::launch_pir_fold_sliced((const uint32_t*)bits_sgm, wpk, (const uint8_t*)dbs, nrec, nkeys,
+                                            (uint32_t*)ans, (uint32_t*)parts, 0, nkeys));
+        else if (mfma)
             CK(dpfk::launch_pir_fold_sliced((const uint32_t*)bits, wpk, (const uint8_t*)dbs, nrec, nkeys,
                                             (uint32_t*)ans, (uint32_t*)parts, 0));
         else

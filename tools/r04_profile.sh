@@ -22,4 +22,7 @@ for w in eval split pir; do
   echo "pmc $w done"
 done
 { command -v go && go version; } > "gpurun_out/$T/go_probe.txt" 2>&1 || echo "go: not found on the GPU box ($(date -u +%FT%TZ))" > "gpurun_out/$T/go_probe.txt"
+# Keep summaries, drop the per-dispatch CSVs (gpurun copies back at most 64 MiB).
+find "gpurun_out/$T" \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" -o -name "*agent_info.csv" \) -delete
+du -sh "gpurun_out/$T"
 echo "round profile done"
