@@ -43,9 +43,6 @@
 #ifndef DPF_DEPTH_MODEL_COOP
 #define DPF_DEPTH_MODEL_COOP 1   // pick_shape prices the shared walk (latency once + W - 6 per thread)
 #endif
-#ifndef DPF_COOP_EXTRA
-#define DPF_COOP_EXTRA 0   // levels wave 0 expands below its 64 shared-walk nodes (0-2)
-#endif
 #ifndef DPF_WALK_BATCH
 #define DPF_WALK_BATCH 1   // tree kernels' root-to-subtree walks: batched single-block rounds
 #endif
@@ -485,14 +482,10 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
         // threads) and leaves them in LDS; every thread then walks only the
         // last W - 6 levels.  Wave-AES per workgroup: l1 + (B/64)(W - 6)
         // instead of (B/64) ltop (configs[4]: 33 vs 96, configs[3]: 39 vs 144).
-        // DPF_COOP_EXTRA = e: wave 0 then expands its 64 nodes e more levels
-        // (64 * 2^e nodes; e expand steps of latency, independent pairs), and
-        // every thread walks W - 6 - e levels instead.
-        constexpr uint32_t E = DPF_COOP_EXTRA;
-        __shared__ uint32_t s_front[(64 << E) * 5];
+        __shared__ uint32_t s_front[64 * 5];
         const uint32_t B = blockDim.x;
         const uint32_t W = 31u - (uint32_t)__builtin_clz(B);
-        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 + E && units_log >= W) {   // uniform over the workgroup
+        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W) {   // uniform over the workgroup
             const uint32_t l1 = ltop - W + 6;
             if (threadIdx.x < 64) {
                 const uint64_t subj = (sub - threadIdx.x) + ((uint64_t)threadIdx.x << (W - 6));
@@ -501,35 +494,14 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
                     CW cw = key_cw<RAW>(c.ks, i);
                     walk_step<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
                 }
-                auto put = [&](uint32_t q, const Node& x) {
-                    uint32_t* f = s_front + 5 * q;
-                    f[0] = x.s.c0; f[1] = x.s.c1; f[2] = x.s.c2; f[3] = x.s.c3; f[4] = x.t;
-                };
-                if constexpr (E == 0) {
-                    put(threadIdx.x, m);
-                } else {
-                    Node L, R;
-                    expand<DPF_WALK_BATCH>(c.tab, c.lo, m, key_cw<RAW>(c.ks, l1), L, R);
-                    if constexpr (E == 1) {
-                        put(2 * threadIdx.x, L);
-                        put(2 * threadIdx.x + 1, R);
-                    } else {
-                        const CW cw1 = key_cw<RAW>(c.ks, l1 + 1);
-                        Node a, b, d, e;
-                        expand<DPF_WALK_BATCH>(c.tab, c.lo, L, cw1, a, b);
-                        expand<DPF_WALK_BATCH>(c.tab, c.lo, R, cw1, d, e);
-                        put(4 * threadIdx.x, a);
-                        put(4 * threadIdx.x + 1, b);
-                        put(4 * threadIdx.x + 2, d);
-                        put(4 * threadIdx.x + 3, e);
-                    }
-                }
+                uint32_t* f = s_front + 5 * threadIdx.x;
+                f[0] = m.s.c0; f[1] = m.s.c1; f[2] = m.s.c2; f[3] = m.s.c3; f[4] = m.t;
             }
             __syncthreads();
-            const uint32_t* f = s_front + 5 * (threadIdx.x >> (W - 6 - E));
+            const uint32_t* f = s_front + 5 * (threadIdx.x >> (W - 6));
             n.s = {f[0], f[1], f[2], f[3]};
             n.t = f[4];
-            lvl = l1 + E;
+            lvl = l1;
         }
     }
     for (uint32_t i = lvl; i < ltop; ++i) {
