@@ -314,11 +314,21 @@ class Ctx:
             dpf.set_aes_impl(args.aes)
         self.stream = torch.cuda.current_stream(self.dev)
 
-    def timed(self, step, steps, warmup):
+    def timed(self, step, steps, warmup, every=None):
         """Warmup, then `steps` steps between barrier+sync pairs; returns the
         max-over-ranks wall time and the mean kernel time of the event pairs."""
         torch, dist = self.torch, self.dist
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        # Kernel time is sampled: events bracket every n-th step (--event-every,
+        # default 10).  A timing event is a barrier packet in the queue; on every
+        # step it cost ~8 us/step (0.1431 vs 0.1350 ms at 512 keys, 0.953 vs
+        # 0.943 ms at 4096: profiles/r04/events), which the wall clock would
+        # then charge to the path.  At least 5 samples per timed region;
+        # n=0: no events (kernel_ms NaN).
+        if every is None:
+            every = self.args.event_every
+            every = max(1, min(every, steps // 5)) if every > 0 else 0
+        timed_i = [i for i in range(steps) if every > 0 and i % every == 0]
         # Clock spin-up (untimed, before the W warmup steps): an idle MI355X
         # needs a few hundred ms of load to reach its steady-state clock; a
         # 5-step warmup (~6 ms) left configs[1] at 1.174 ms/launch against
@@ -348,7 +358,7 @@ class Ctx:
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
         for i in range(steps):
-            step(evs[i])
+            step(evs[i] if every == 1 or i in timed_i else None)
         torch.cuda.synchronize(self.dev)
         if self.world > 1:
             dist.barrier()
@@ -358,12 +368,12 @@ class Ctx:
                              device=self.dev if self.backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             t_wall = float(t.item())
-        k_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+        k_ms = (sum(evs[i][0].elapsed_time(evs[i][1]) for i in timed_i) / len(timed_i)) if timed_i else float("nan")
         return t_wall, k_ms
 
     def line(self, **kw):
         base = {"n_gpus": self.world, "steps": self.args.steps, "warmup": self.args.warmup,
-                "spinup_s": self.args.spinup,
+                "spinup_s": self.args.spinup, "event_every": self.args.event_every,
                 "higher_is_better": True, "vs_baseline": None, "dtype": "u32"}
         base.update(kw)
         return base
@@ -746,8 +756,8 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
         if ev:
             ev[1].record(c.stream)
 
-    _, t_ms = c.timed(tree, steps, 3)
-    _, f_ms = c.timed(fold, steps, 3)
+    _, t_ms = c.timed(tree, steps, 3, every=1)      # kernel times only: events on every step
+    _, f_ms = c.timed(fold, steps, 3, every=1)
     # The same two phases back to back, as in a step, with an event between
     # them: each phase's time when it follows the other.
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
@@ -939,6 +949,8 @@ def main() -> None:
                     help="pir: XOR fold on the matrix cores over the bit-sliced DB (default) or the LDS fold")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="split/pir on 1 GPU: time rank 0's share of a W-way split")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="record kernel timing events on every n-th timed step (1 = every step, 0 = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--aes", choices=["ttable", "bitsliced"], default=None,
                     help="tree-kernel AES back end for the headline (default: the library's)")
