@@ -127,7 +127,7 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
                     t = json.load(f)
             except Exception:
                 continue
-            # PIR: the roofline is the tree's (k_unpack + k_evalfull); the fold has its
+            # PIR: the roofline is the tree's (k_evalfull); the fold has its
             # own, and k_slice_db runs once per DB load, not per step.
             ks = sorted(k for k in t if k.startswith("k_") and not k.startswith("k_slice")
                         and (workload != "pir" or not k.startswith(("k_fold", "k_xor"))))
@@ -791,7 +791,7 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
                 break
     return {"back_to_back": in_step,
             "tree": {"kernel_ms": round(t_ms, 4), "aes_blocks_per_s": blocks / (t_ms * 1e-3),
-                     "kernels": "k_unpack + k_evalfull"},
+                     "kernels": "k_evalfull (key bytes read in place; k_unpack first where a wave does not own a key)"},
             "fold": {"kernel_ms": round(f_ms, 4),
                      "kernels": ("k_fold_mfma / k_fold_sliced_direct (bit-sliced DB)" if c.args.pir_fold == "mfma"
                                  else "k_fold_direct / k_fold4r (row-major DB)") + " + k_xor_parts",
@@ -835,7 +835,7 @@ def wl_pir(c: Ctx) -> dict:
     # apart below, and the top-level roofline is the tree's own.
     kern = pir_breakdown(c, W, d_db, lo, hi, nk, min(a.steps, 20))
     line["kernels"] = kern
-    line["roofline"] = prg_roofline(aes / (kern["tree"]["kernel_ms"] * 1e-3), "k_unpack+k_evalfull (PIR tree)",
+    line["roofline"] = prg_roofline(aes / (kern["tree"]["kernel_ms"] * 1e-3), "k_evalfull (PIR tree)",
                                     kern["tree"]["kernel_ms"], nk * ((hi - lo) // 8), workload="pir",
                                     profiled_shape=(W == 1 and nk == 64))
     line["roofline"]["step_kernel_ms"] = round(k_ms, 4)
