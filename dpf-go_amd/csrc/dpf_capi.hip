@@ -679,6 +679,13 @@ int dpf_set_aes_impl(int impl) {
 
 int dpf_get_aes_impl(void) { return g_aes_impl.load(); }
 
+int dpf_set_eval_kernel(int kernel) {
+    if (kernel != DPF_EVAL_WALK && kernel != DPF_EVAL_TRIE) return fail(DPF_ERR_PARAM, "dpf: unknown Eval kernel");
+    return dpfk::set_eval_trie(kernel == DPF_EVAL_TRIE) ? DPF_EVAL_TRIE : DPF_EVAL_WALK;
+}
+
+int dpf_get_eval_kernel(void) { return dpfk::get_eval_trie() ? DPF_EVAL_TRIE : DPF_EVAL_WALK; }
+
 int dpf_aes_mmo_dev(int device, int impl, int right, const uint8_t* d_in, uint8_t* d_out, size_t nblocks,
                     uint32_t reps, void* stream) {
     if (impl != DPF_AES_TTABLE && impl != DPF_AES_BITSLICED) return fail(DPF_ERR_PARAM, "dpf: unknown AES back end");

@@ -14,6 +14,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include "aes_consts.hpp"
 #include "aes_ttable.hpp"
@@ -682,6 +683,200 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
     }
 }
 
+// Batched Eval as a visited-node trie below the frontier.
+// A key's queries share prefixes: at configs[2] (1024 points per key,
+// stop 13) levels 10-13 hold only 647 / 806 / 906 / 963 distinct nodes and
+// 963 distinct leaf blocks, where per-query walks compute 1024 of each.
+// One 1024-thread workgroup (the CU's LDS: one 64 KiB table plus the trie
+// state) takes kTrieKeys keys:
+//   1. every query marks its node at each level L..stop in per-level bitmaps
+//      (LDS atomics), and one wave per (key, level) turns a bitmap into
+//      per-word prefix counts: rank(pos) = prefix[pos/32] + popc(bits below);
+//   2. the key's visited level-L nodes come from the HBM frontier (the NODES
+//      pass), stored by rank;
+//   3. per level l = L+1..stop, every visited child finds its parent's rank
+//      (map pass: thread per bitmap word, one entry per set bit), then all
+//      children are computed with one AES each (dpf.go:183-201's on-path
+//      child), reading every parent before any child overwrites the store;
+//      at l = stop the leaf MMO follows at once (dpf.go:214-224);
+//   4. each query reads bit x & 127 of its leaf block by rank.
+// AES per key at configs[2]: 1022 (frontier) + 4285 = 5307, against 6142
+// for frontier + per-query walks.  Output: one 0/1 byte per query, as k_eval.
+constexpr uint32_t kTrieKeys = 4;           // keys per workgroup
+constexpr uint32_t kTrieCap = 1024;         // nodes per key per level (pts_per_key <= kTrieCap)
+constexpr uint32_t kTrieBlock = 1024;       // threads per workgroup (16 waves: 4 per SIMD)
+constexpr uint32_t kTrieMaxStop = 13;       // bitmaps: 2^l bits per level l <= 13
+constexpr uint32_t kTrieWords = 520;        // bitmap words per key, levels L..stop (<= 2^(stop-4) + levels)
+constexpr uint32_t kTrieItems = kTrieKeys * kTrieCap / kTrieBlock;   // children per thread per level (4)
+
+__device__ __forceinline__ uint32_t trie_words(uint32_t l) { return l >= 5 ? 1u << (l - 5) : 1u; }
+
+__global__ __launch_bounds__(kTrieBlock, 1) void k_eval_trie(const uint32_t* __restrict__ ekeys, uint32_t stop,
+                                                              uint32_t logN, const uint64_t* __restrict__ xs,
+                                                              uint64_t nkeys, uint32_t ppk,
+                                                              const uint4* __restrict__ fseed,
+                                                              const uint8_t* __restrict__ ft, uint32_t L,
+                                                              uint8_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+    __shared__ __attribute__((aligned(16))) uint4 s_node[kTrieKeys * kTrieCap];   // seeds (leaf blocks at the end)
+    __shared__ uint8_t s_t[kTrieKeys * kTrieCap];
+    __shared__ uint16_t s_map[kTrieKeys * kTrieCap];                              // parent rank * 2 + side
+    __shared__ uint32_t s_bm[kTrieKeys * kTrieWords];
+    __shared__ uint16_t s_pre[kTrieKeys * kTrieWords];
+    __shared__ uint32_t s_cnt[kTrieKeys][kTrieMaxStop + 2];                       // visited nodes per level
+    const uint32_t tid = threadIdx.x;
+    const uint64_t k0 = (uint64_t)blockIdx.x * kTrieKeys;
+    const uint32_t nk = (uint32_t)(nkeys - k0 < kTrieKeys ? nkeys - k0 : kTrieKeys);
+    const uint32_t npts = nk * ppk;
+    const uint64_t q0 = k0 * ppk;
+    // Word offset of level l's bitmap inside a key's kTrieWords.
+    auto woff = [&](uint32_t l) {
+        uint32_t o = 0;
+        for (uint32_t i = L; i < l; ++i) o += trie_words(i);
+        return o;
+    };
+    auto pos_at = [&](uint64_t x, uint32_t l) { return (uint32_t)(x >> (logN - l)) & ((1u << l) - 1u); };
+    auto rank = [&](uint32_t k, uint32_t wo, uint32_t p) {
+        const uint32_t w = k * kTrieWords + wo + (p >> 5);
+        return (uint32_t)s_pre[w] + (uint32_t)__builtin_popcount(s_bm[w] & ((1u << (p & 31)) - 1u));
+    };
+    for (uint32_t i = tid; i < kTrieKeys * kTrieWords; i += kTrieBlock) s_bm[i] = 0;
+    fill_table(s_tab);                                   // ends with a barrier
+    // 1. Mark every query's node at each level L..stop.
+    for (uint32_t i = tid; i < npts; i += kTrieBlock) {
+        const uint64_t x = xs[q0 + i];
+        const uint32_t k = i / ppk;
+        uint32_t wo = 0;
+        for (uint32_t l = L; l <= stop; ++l) {
+            const uint32_t p = pos_at(x, l);
+            atomicOr(&s_bm[k * kTrieWords + wo + (p >> 5)], 1u << (p & 31));
+            wo += trie_words(l);
+        }
+    }
+    __syncthreads();
+    {   // Prefix counts: one wave per (key, level) segment.
+        const uint32_t wave = tid >> 6, lane = tid & 63, nlev = stop - L + 1;
+        for (uint32_t sg = wave; sg < nk * nlev; sg += kTrieBlock / 64) {
+            const uint32_t k = sg / nlev, l = L + sg % nlev;
+            const uint32_t base = k * kTrieWords + woff(l), nw = trie_words(l);
+            uint32_t carry = 0;
+            for (uint32_t c = 0; c < nw; c += 64) {
+                const uint32_t w = c + lane;
+                const uint32_t v = w < nw ? (uint32_t)__builtin_popcount(s_bm[base + w]) : 0u;
+                uint32_t inc = v;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t o = __shfl_up(inc, d, 64);
+                    if (lane >= (uint32_t)d) inc += o;
+                }
+                if (w < nw) s_pre[base + w] = (uint16_t)(carry + inc - v);
+                carry += __shfl(inc, 63, 64);
+            }
+            if (lane == 0) s_cnt[k][l - L] = carry;
+        }
+    }
+    __syncthreads();
+    // 2. The visited level-L nodes, by rank, from the HBM frontier.
+    for (uint32_t i = tid; i < (nk << L); i += kTrieBlock) {
+        const uint32_t k = i >> L, p = i & ((1u << L) - 1u);
+        const uint32_t w = k * kTrieWords + (p >> 5);
+        if ((s_bm[w] >> (p & 31)) & 1u) {
+            const uint32_t r = rank(k, 0, p);
+            const uint64_t idx = ((k0 + k) << L) + p;
+            s_node[k * kTrieCap + r] = fseed[idx];
+            s_t[k * kTrieCap + r] = ft[idx];
+        }
+    }
+    const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
+    const uint32_t lo = (tid & 31u) * 4u;
+    const uint64_t rec = (uint64_t)(stop + 2) * 8;
+    uint32_t wo_par = 0;
+    for (uint32_t l = L + 1; l <= stop; ++l) {
+        const uint32_t wo = wo_par + trie_words(l - 1), nw = trie_words(l);
+        // 3a. Map pass: child rank -> parent rank * 2 + side.
+        for (uint32_t i = tid; i < nk * nw; i += kTrieBlock) {
+            const uint32_t k = i / nw, w = i % nw;
+            uint32_t bits = s_bm[k * kTrieWords + wo + w];
+            uint32_t r = s_pre[k * kTrieWords + wo + w];
+            while (bits) {
+                const uint32_t b = (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1u;
+                const uint32_t c = 32u * w + b;
+                s_map[k * kTrieCap + r++] = (uint16_t)((rank(k, wo_par, c >> 1) << 1) | (c & 1u));
+            }
+        }
+        __syncthreads();
+        // 3b. Children: read every parent, then compute and store.
+        uint32_t off[kTrieKeys + 1];
+        off[0] = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kTrieKeys; ++k) off[k + 1] = off[k] + (k < nk ? s_cnt[k][l - L] : 0u);
+        Node n[kTrieItems];
+        uint32_t kk[kTrieItems], jj[kTrieItems], side[kTrieItems];
+#pragma unroll
+        for (uint32_t m = 0; m < kTrieItems; ++m) {
+            const uint32_t i = tid + m * kTrieBlock;
+            uint32_t k = 0;
+#pragma unroll
+            for (uint32_t z = 1; z < kTrieKeys; ++z) k += i >= off[z] ? 1u : 0u;
+            kk[m] = k;
+            jj[m] = i - off[k];
+            side[m] = 0;
+            n[m] = {{0, 0, 0, 0}, 0};
+            if (i < off[kTrieKeys]) {
+                const uint32_t v = s_map[k * kTrieCap + jj[m]];
+                const uint4 sd = s_node[k * kTrieCap + (v >> 1)];
+                n[m] = {{sd.x, sd.y, sd.z, sd.w}, s_t[k * kTrieCap + (v >> 1)]};
+                side[m] = v & 1u;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t m = 0; m < kTrieItems; m += 2) {
+            const uint32_t ia = tid + m * kTrieBlock, ib = ia + kTrieBlock;
+            if (ia >= off[kTrieKeys]) break;                       // ib >= ia: both past the end
+            const uint32_t* eka = ekeys + (k0 + kk[m]) * rec;
+            const uint32_t* ekb = ekeys + (k0 + kk[m + 1]) * rec;
+            const bool hb = ib < off[kTrieKeys];
+            // Valid items are the first off[kTrieKeys] of the level, so only
+            // one wave per slot pair is ragged: waves without a second item
+            // run one AES instead of two (the saving is per wave instruction).
+            if (__builtin_amdgcn_read_exec() & __ballot(hb)) {
+                walk_step2<DPF_EVAL_BATCH>(tab, lo, n[m], load_cw(eka, l - 1), side[m], n[m + 1],
+                                           load_cw(hb ? ekb : eka, l - 1), side[m + 1]);
+                if (l == stop) {                                   // leaf blocks (dpf.go:214-224)
+                    Blk oa, ob;
+                    mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n[m].s, oa, KeyFixed<false>{}, n[m + 1].s, ob);
+                    n[m].s = leaf_fix(oa, n[m].t, load_blk(eka + 8 + 8 * stop));
+                    n[m + 1].s = leaf_fix(ob, n[m + 1].t, load_blk((hb ? ekb : eka) + 8 + 8 * stop));
+                }
+            } else {
+                walk_step<DPF_EVAL_BATCH>(tab, lo, n[m], load_cw(eka, l - 1), side[m]);
+                if (l == stop)
+                    n[m].s = leaf_fix(mmo1<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n[m].s), n[m].t,
+                                      load_blk(eka + 8 + 8 * stop));
+            }
+            s_node[kk[m] * kTrieCap + jj[m]] = make_uint4(n[m].s.c0, n[m].s.c1, n[m].s.c2, n[m].s.c3);
+            s_t[kk[m] * kTrieCap + jj[m]] = (uint8_t)n[m].t;
+            if (hb) {
+                s_node[kk[m + 1] * kTrieCap + jj[m + 1]] =
+                    make_uint4(n[m + 1].s.c0, n[m + 1].s.c1, n[m + 1].s.c2, n[m + 1].s.c3);
+                s_t[kk[m + 1] * kTrieCap + jj[m + 1]] = (uint8_t)n[m + 1].t;
+            }
+        }
+        wo_par = wo;
+        __syncthreads();   // children stored before the next map pass's parents are read (3b)
+    }
+    // 4. Each query's bit of its leaf block.
+    for (uint32_t i = tid; i < npts; i += kTrieBlock) {
+        const uint64_t x = xs[q0 + i];
+        const uint32_t k = i / ppk;
+        const uint32_t r = rank(k, wo_par, pos_at(x, stop));
+        const uint4 o = s_node[k * kTrieCap + r];
+        out[q0 + i] = eval_bit({o.x, o.y, o.z, o.w}, x);
+    }
+}
+
 // aes128MMO microbenchmark / self-test on the T-table back end: two
 // independent blocks per thread (the PRG's own ILP), iterated `reps` times.
 template <bool RIGHT>
@@ -913,6 +1108,24 @@ uint64_t eval_frontier_bytes(uint64_t nkeys, uint32_t stop, uint64_t pts_per_key
     return ((nkeys << L) * 16 + (nkeys << L) + 255) & ~255ull;
 }
 
+// The trie kernel's limits: every level's bitmap and nodes in LDS.
+static bool trie_ok(uint32_t stop, uint32_t logN, uint64_t ppk, uint32_t L) {
+    if (L < 4 || L >= stop || stop > kTrieMaxStop || logN != stop + 7 || ppk == 0 || ppk > kTrieCap) return false;
+    uint32_t w = 0;
+    for (uint32_t l = L; l <= stop; ++l) w += l >= 5 ? 1u << (l - 5) : 1u;
+    return w <= kTrieWords;
+}
+// Batched Eval kernel (dpf_set_eval_kernel): 0 = frontier + per-query walks
+// (default), 1 = the trie kernel where trie_ok holds.  Env DPF_EVAL_TRIE=1
+// sets the initial value.
+static std::atomic<int> g_eval_trie{[] {
+    const char* e = getenv("DPF_EVAL_TRIE");
+    return e && e[0] == '1' ? 1 : 0;
+}()};
+static bool trie_on() { return g_eval_trie.load(std::memory_order_relaxed) != 0; }
+int set_eval_trie(int on) { return g_eval_trie.exchange(on ? 1 : 0); }
+int get_eval_trie() { return g_eval_trie.load(); }
+
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
                        uint64_t pts_per_key, uint8_t* out, void* frontier, uint64_t frontier_bytes,
                        hipStream_t st) {
@@ -934,6 +1147,12 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
         if (e != hipSuccess) return e;
         fseed = reinterpret_cast<const uint4*>(fs);
         ft = fts;
+    }
+    if (L > 0 && trie_on() && trie_ok(stop, logN, pts_per_key, L)) {
+        const uint64_t blocks = (nkeys + kTrieKeys - 1) / kTrieKeys;
+        hipLaunchKernelGGL(k_eval_trie, dim3((uint32_t)blocks), dim3(kTrieBlock), 0, st, ek, stop, logN, xs, nkeys,
+                           (uint32_t)pts_per_key, fseed, ft, L, out);
+        return hipGetLastError();
     }
 #if DPF_EVAL_PAIRS
     const uint64_t nthreads = (nq + 1) / 2;

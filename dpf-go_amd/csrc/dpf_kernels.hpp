@@ -54,6 +54,9 @@ hipError_t launch_nodes(const uint32_t* ek, uint64_t nkeys, uint32_t stop, uint3
 // computed into `frontier` (eval_frontier_bytes of it) and each query starts
 // there; with frontier == nullptr (or too small) every walk starts at the root.
 uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key);
+// Batched Eval kernel choice: 1 = visited-node trie below the frontier.
+int set_eval_trie(int on);   // returns the previous choice
+int get_eval_trie();
 uint64_t eval_frontier_bytes(uint64_t nkeys, uint32_t stop, uint64_t pts_per_key);
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
                        uint64_t pts_per_key, uint8_t* out, void* frontier, uint64_t frontier_bytes,

@@ -85,6 +85,8 @@ SIGNATURES = {
     "dpf_small_call_max_logN": (ctypes.c_uint32, []),
     "dpf_set_aes_impl": (_int, [_int]),
     "dpf_get_aes_impl": (_int, []),
+    "dpf_set_eval_kernel": (_int, [_int]),
+    "dpf_get_eval_kernel": (_int, []),
     "dpf_aes_mmo_dev": (_int, [_int, _int, _int, _vp, _vp, _sz, _u32, _vp]),
     "dpf_xor_fold_workspace_size": (_sz, []),
     "dpf_xor_fold_dev": (_int, [_int, _vp, _sz, _sz, _vp, _u64, _sz, _vp, _vp, _vp]),
@@ -382,6 +384,23 @@ def set_aes_impl(impl) -> int:
 
 def get_aes_impl() -> int:
     return int(lib().dpf_get_aes_impl())
+
+
+EVAL_WALK, EVAL_TRIE = 0, 1
+
+
+def set_eval_kernel(kernel) -> int:
+    """Select the batched Eval kernel ("walk"/"trie" or 0/1); returns the previous one."""
+    if isinstance(kernel, str):
+        kernel = {"walk": EVAL_WALK, "trie": EVAL_TRIE}[kernel]
+    rc = lib().dpf_set_eval_kernel(kernel)
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+def get_eval_kernel() -> int:
+    return int(lib().dpf_get_eval_kernel())
 
 
 SMALL_AUTO, SMALL_GPU, SMALL_HOST = 0, 1, 2

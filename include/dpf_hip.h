@@ -150,6 +150,17 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t
 #define DPF_AES_BITSLICED 1
 int dpf_set_aes_impl(int impl);   /* returns the previous back end */
 int dpf_get_aes_impl(void);
+/* ---- batched Eval kernel (dpf_eval_batch*, BASELINE configs[2]) ---------
+ * DPF_EVAL_WALK (default): the level-L frontier, then one walk per query.
+ * DPF_EVAL_TRIE: the same frontier, then only the visited nodes of each
+ * key's query trie below it (5,307 instead of 6,142 AES per
+ * key at configs[2]), where logN <= 20 and pts_per_key <= 1024; the walk
+ * kernel elsewhere.  Outputs are bit-identical.  Process-wide; env
+ * DPF_EVAL_TRIE=1 sets the initial value. */
+#define DPF_EVAL_WALK 0
+#define DPF_EVAL_TRIE 1
+int dpf_set_eval_kernel(int kernel);   /* returns the previous kernel */
+int dpf_get_eval_kernel(void);
 /* ---- small-call path of the single-key API ---------------
  * dpf_eval and dpf_evalfull are the reference's latency-bound single calls
  * (dpf.go:171, :243).  DPF_SMALL_AUTO (default) evaluates them on the host's

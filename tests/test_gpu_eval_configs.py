@@ -155,3 +155,43 @@ def test_logN32_dense_oracle_sample():
     for blk, xx in ((head, xs_h), (tail, xs_t)):
         w = oracle.eval_batch(ka, xx.reshape(1, -1), logN, nthreads=NT)[0]
         assert np.array_equal(np.unpackbits(blk, bitorder="little"), w)
+
+
+@pytest.fixture()
+def trie_kernel():
+    prev = dpf.set_eval_kernel("trie")
+    yield
+    dpf.set_eval_kernel(prev)
+
+
+def test_config2_trie_kernel_full_size(cfg2, trie_kernel):
+    """configs[2] through the visited-node trie kernel (DPF_EVAL_TRIE):
+    every query by the share property, 512 keys against the oracle."""
+    logN, al, ka, kb, xs, pos = cfg2
+    assert dpf.get_eval_kernel() == dpf.EVAL_TRIE
+    got_a = dpf.eval_batch(ka, xs, logN, ngpus=1)
+    got_b = dpf.eval_batch(kb, xs, logN, ngpus=1)
+    _check_cfg2(got_a, got_b, cfg2)
+
+
+@pytest.mark.parametrize("logN,nk,ppk", [(20, 4097, 1024), (16, 9, 1000), (20, 6, 64), (14, 5, 256),
+                                         (12, 7, 64), (18, 3, 777)])
+def test_trie_kernel_shapes(logN, nk, ppk, trie_kernel):
+    """The trie kernel at ragged shapes: a last workgroup with fewer than 4
+    keys, non-power-of-two points per key, the shallowest frontier (L = 4),
+    duplicate points, x >= 2^logN and every key's alpha among its points;
+    equal to the oracle and to the walk kernel."""
+    rng = np.random.default_rng(logN * 1000 + ppk)
+    al, ka, kb = _keys(nk, logN, first=70000 + nk + ppk)
+    xs = synth.eval_points(nk, ppk, logN, master=0x7E1E + ppk)
+    xs[:, 1] = al
+    xs[:, 2] = xs[:, 3]                                          # duplicates
+    xs[:, 4] = al | (np.uint64(1) << np.uint64(40))              # beyond the domain, same leaf bit
+    xs[:, 5:9] = (al[:, None] ^ np.uint64(1)) & np.uint64((1 << logN) - 1)   # the alpha leaf block's neighbours
+    xs[:, 9] = rng.integers(0, 2 ** 63, size=nk, dtype=np.uint64)
+    for k in (ka, kb):
+        got = dpf.eval_batch(k, xs, logN, ngpus=1)
+        want = oracle.eval_batch(k, xs, logN, nthreads=NT)
+        assert np.array_equal(got, want), (logN, nk, ppk)
+    dpf.set_eval_kernel("walk")
+    assert np.array_equal(dpf.eval_batch(ka, xs, logN, ngpus=1), oracle.eval_batch(ka, xs, logN, nthreads=NT))
