@@ -207,3 +207,25 @@ func GetSmallCallPath() int {
 func SmallCallMaxLogN() uint64 {
 	return uint64(C.dpf_small_call_max_logN())
 }
+
+// Batched Eval kernel (include/dpf_hip.h DPF_EVAL_*): EvalWalk (default)
+// walks each query from the shared frontier, EvalTrie computes only the
+// visited nodes of each key's query trie (logN <= 20, <= 1024 points per
+// key; bit-identical, measured slower on MI355X).  Returns the previous one.
+const (
+	EvalWalk = 0
+	EvalTrie = 1
+)
+
+func SetEvalKernel(kernel int) int {
+	rc := C.dpf_set_eval_kernel(C.int(kernel))
+	if rc < 0 {
+		check(rc)
+	}
+	return int(rc)
+}
+
+// GetEvalKernel returns the current batched Eval kernel (dpf_get_eval_kernel).
+func GetEvalKernel() int {
+	return int(C.dpf_get_eval_kernel())
+}
