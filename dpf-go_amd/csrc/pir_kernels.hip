@@ -703,10 +703,11 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 #endif
 // KG key groups per workgroup: wave w takes bit slice w % (8/NT) of key
 // group w / (8/NT), so a workgroup covers 32*MT*KG keys x 256 bits.
-// SGM: the selection bits are super-group-major, sel[S][sgm_keys][8 words]
-// (a staged block is then one contiguous read per super-group) instead of
-// EvalFull's key-major [key][wpk words].
-template <int MT, int NT, int SG, int KG, bool SGM = false>
+// SGM: the selection bits are super-group-major in chunks of G super-groups,
+// sel[S / G][sgm_keys][G * 8 words] (G = sgm_g: 1, or 4 = one 128-byte line
+// of a key per chunk, as the PIR tree kernel writes them), so a staged block
+// is one contiguous region instead of EvalFull's key-major [key][wpk words].
+template <int MT, int NT, int SG, int KG, int SGM = 0>
 __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
@@ -730,7 +731,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
     // Piece p -> (row, q = 16-byte piece of the row's block span): key-major,
     // row = p / 2SG; super-group-major, p = (s * kRows + row) * 2 + half.
     auto piece = [&](uint32_t p, uint32_t& row, uint32_t& q) __attribute__((always_inline)) {
-        if constexpr (SGM) {
+        if constexpr (SGM == 1) {
             row = (p >> 1) % kRows;
             q = 2 * ((p >> 1) / kRows) + (p & 1);
         } else {
@@ -746,7 +747,9 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
             piece(p, row, q);
             const uint64_t word = sb * 8 + 4 * q;
             const bool ok = p < (uint32_t)kPieces && row < nkeys && word + 4 <= wpk;
-            const uint64_t at = SGM ? ((sb + q / 2) * sgm_keys + row) * 8 + 4 * (q & 1) : (uint64_t)row * wpk + word;
+            const uint64_t S = sb + q / 2;
+            const uint64_t at = SGM ? ((S / SGM * sgm_keys + row) * SGM + S % SGM) * 8 + 4 * (q & 1)
+                                    : (uint64_t)row * wpk + word;
             const uint4 x = *reinterpret_cast<const uint4*>(bits + (ok ? at : 0));
             v[i] = ok ? x : make_uint4(0, 0, 0, 0);
         }
@@ -979,7 +982,7 @@ namespace {
 template <int MT, int NT, int SG, int KG>
 hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
                           uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st,
-                          uint32_t sgm_keys = 0) {
+                          uint32_t sgm_keys = 0, uint32_t sgm_g = 1) {
     constexpr int NW = 8 / NT * KG;
     // Resident workgroups only (one round): each takes a contiguous run of
     // whole staged blocks.  (A fixed 4 workgroups per CU left 1/4 - 3/4 of
@@ -992,8 +995,11 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
     }();
     uint64_t spb;
     split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
-    if (sgm_keys)
-        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, true>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+    if (sgm_keys && sgm_g == 4)
+        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 4>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, sgm_keys);
+    else if (sgm_keys)
+        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 1>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
                            reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, sgm_keys);
     else
         hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
@@ -1015,7 +1021,8 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
 #define DPF_FOLD_SHAPE64 0   // 33-64 keys
 #endif
 hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
-                                  uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st, uint32_t sgm_keys) {
+                                  uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st, uint32_t sgm_keys,
+                                  uint32_t sgm_g) {
     if (nkeys == 0) return hipSuccess;
     if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * 32, st);
     if (words_per_key % 4 != 0 || words_per_key * 32 < nrec) return hipErrorInvalidValue;
@@ -1034,30 +1041,30 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
     }
     for (uint32_t k0 = 0; k0 < nkeys; k0 += 256) {
         const uint32_t nk = nkeys - k0 < 256 ? nkeys - k0 : 256;
-        const uint32_t* b = bits + (sgm_keys ? (uint64_t)k0 * 8 : (uint64_t)k0 * words_per_key);
+        const uint32_t* b = bits + (sgm_keys ? (uint64_t)k0 * 8 * sgm_g : (uint64_t)k0 * words_per_key);
         uint32_t* zero = k0 == 0 ? ans : nullptr;
         const uint64_t zw = k0 == 0 ? (uint64_t)nkeys * 8 : 0;
         uint64_t blocks = 0;
         uint32_t mt;
         hipError_t e;
-        if (nk <= 32) e = launch_mfma_mt<1, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys), mt = 1;
+        if (nk <= 32) e = launch_mfma_mt<1, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g), mt = 1;
         else if (nk <= 64) {
             mt = 2;
-            if (DPF_FOLD_SHAPE64 == 1) e = launch_mfma_mt<2, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
-            else if (DPF_FOLD_SHAPE64 == 2) e = launch_mfma_mt<1, 2, 4, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
-            else if (DPF_FOLD_SHAPE64 == 3) e = launch_mfma_mt<2, 4, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
-            else e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            if (DPF_FOLD_SHAPE64 == 1) e = launch_mfma_mt<2, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            else if (DPF_FOLD_SHAPE64 == 2) e = launch_mfma_mt<1, 2, 4, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            else if (DPF_FOLD_SHAPE64 == 3) e = launch_mfma_mt<2, 4, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            else e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
         }
         else if (nk <= 128) {
             mt = 4;
-            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
-            else e = launch_mfma_mt<4, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            else e = launch_mfma_mt<4, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
         } else {
             mt = 8;
-            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
-            else if (DPF_FOLD_SHAPE == 2) e = launch_mfma_mt<4, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
-            else if (DPF_FOLD_SHAPE == 3) e = launch_mfma_mt<2, 8, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
-            else e = launch_mfma_mt<8, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys);
+            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            else if (DPF_FOLD_SHAPE == 2) e = launch_mfma_mt<4, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            else if (DPF_FOLD_SHAPE == 3) e = launch_mfma_mt<2, 8, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            else e = launch_mfma_mt<8, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
         }
         if (e != hipSuccess) return e;
         const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);

@@ -34,10 +34,11 @@ hipError_t launch_pir_fold(const uint32_t* bits, uint64_t words_per_key, const u
 // as launch_pir_fold.
 uint64_t pir_sliced_bytes(uint64_t nrec);
 hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipStream_t st);
-// sgm_keys > 0: the selection bits are super-group-major instead,
-// bits[S][sgm_keys][8 words] (S < ceil(nrec / 256)); key k of the batch is row k.
+// sgm_keys > 0: the selection bits are super-group-major instead, in chunks
+// of sgm_g (1 or 4) super-groups: bits[S / g][sgm_keys][g * 8 words]
+// (S < ceil(nrec / 256)); key k of the batch is row k.
 hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, const uint8_t* dbs, uint64_t nrec,
                                   uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st,
-                                  uint32_t sgm_keys = 0);
+                                  uint32_t sgm_keys = 0, uint32_t sgm_g = 1);
 
 }  // namespace dpfk

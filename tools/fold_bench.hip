@@ -60,15 +60,19 @@ int main(int argc, char** argv) {
     }
     // FOLD_SGM=1 (with FOLD_MODE=mfma): the selection bits super-group-major,
     // sgm[S][key][8 words] = bits[key][8S .. 8S+8), as a tree pass could write them.
-    const bool sgm = mfma && getenv("FOLD_SGM") && getenv("FOLD_SGM")[0] == '1';
+    // FOLD_SGM=4: chunks of 4 super-groups, sgm[S/4][key][32 words] (one
+    // 128-byte line of a key per chunk, as the PIR tree kernel writes them).
+    const uint32_t sgm_g = mfma && getenv("FOLD_SGM") ? (uint32_t)atoi(getenv("FOLD_SGM")) : 0;
+    const bool sgm = sgm_g == 1 || sgm_g == 4;
     void* bits_sgm = nullptr;
     if (sgm) {
-        const uint64_t nsgs = (nrec + 255) / 256;
-        std::vector<uint32_t> t(nsgs * nkeys * 8, 0);
+        const uint64_t nsgs = (nrec + 255) / 256, nch = (nsgs + sgm_g - 1) / sgm_g;
+        std::vector<uint32_t> t(nch * sgm_g * nkeys * 8, 0);
         for (uint64_t S = 0; S < nsgs; ++S)
             for (uint32_t k = 0; k < nkeys; ++k)
                 for (int w = 0; w < 8; ++w)
-                    if (8 * S + w < wpk) t[(S * nkeys + k) * 8 + w] = h[(size_t)k * wpk + 8 * S + w];
+                    if (8 * S + w < wpk)
+                        t[((S / sgm_g * nkeys + k) * sgm_g + S % sgm_g) * 8 + w] = h[(size_t)k * wpk + 8 * S + w];
         CK(hipMalloc(&bits_sgm, t.size() * 4));
         CK(hipMemcpy(bits_sgm, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     }
@@ -76,7 +80,7 @@ int main(int argc, char** argv) {
         CK(hipMemsetAsync(ans, 0, (size_t)nkeys * rec_bytes, 0));
         if (sgm)
             CK(dpfk::launch_pir_fold_sliced((const uint32_t*)bits_sgm, wpk, (const uint8_t*)dbs, nrec, nkeys,
-                                            (uint32_t*)ans, (uint32_t*)parts, 0, nkeys));
+                                            (uint32_t*)ans, (uint32_t*)parts, 0, nkeys, sgm_g));
         else if (mfma)
             CK(dpfk::launch_pir_fold_sliced((const uint32_t*)bits, wpk, (const uint8_t*)dbs, nrec, nkeys,
                                             (uint32_t*)ans, (uint32_t*)parts, 0));
