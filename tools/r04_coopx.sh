@@ -1,6 +1,8 @@
 #!/bin/bash
 # Deeper shared walk (DPF_COOP_EXTRA = 1, 2 variant libs) vs the product lib,
 # interleaved: headline, configs[1] strong per-rank shapes, split and PIR.
+# The macro lives in commit 2752386 (dropped after this A/B: neutral);
+# build the variants there with tools/build_variant.sh coopN "" -DDPF_COOP_EXTRA=N.
 set -uo pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$REPO"

@@ -75,13 +75,19 @@ int main(int argc, char** argv) {
                          (double)(b - t0) * us, (unsigned long long)t[4 * w + 2], (unsigned long long)t[4 * w + 3]);
     }
     if (csv) fclose(csv);
+    std::vector<double> starts;
+    for (uint64_t w = 0; w < dpfk::kWaveTimesMax; ++w)
+        if (t[4 * w + 1]) starts.push_back((double)(t[4 * w] - t0) * us);
+    std::sort(starts.begin(), starts.end());
     std::sort(ends.begin(), ends.end());
     const double span = (double)(t1 - t0) * us;
     auto pct = [&](double p) { return ends.empty() ? 0.0 : ends[(size_t)(p * (ends.size() - 1))]; };
     printf("{\"nkeys\": %llu, \"logN\": %u, \"waves\": %llu, \"event_ms\": %.4f, \"span_us\": %.1f, "
            "\"mean_wave_us\": %.1f, \"end_p0_us\": %.1f, \"end_p10_us\": %.1f, \"end_p50_us\": %.1f, \"end_p90_us\": %.1f, "
-           "\"end_p100_us\": %.1f, \"mean_busy_frac\": %.4f, \"expected_waves\": %llu}\n",
+           "\"end_p100_us\": %.1f, \"start_p50_us\": %.1f, \"start_p100_us\": %.1f, \"mean_busy_frac\": %.4f, "
+           "\"expected_waves\": %llu}\n",
            (unsigned long long)nkeys, logN, (unsigned long long)nwaves, el, span, busy * us / nwaves, pct(0), pct(0.1),
-           pct(0.5), pct(0.9), pct(1.0), busy * us / nwaves / span, (unsigned long long)nw);
+           pct(0.5), pct(0.9), pct(1.0), starts.empty() ? 0.0 : starts[starts.size() / 2],
+           starts.empty() ? 0.0 : starts.back(), busy * us / nwaves / span, (unsigned long long)nw);
     return 0;
 }
