@@ -831,15 +831,34 @@ def wl_pir(c: Ctx) -> dict:
                                       + " (BASELINE configs[4])", "logN": logN, "batch": nk,
                           "parallelism": f"db-shard x{c.world} + all_gather/XOR"},
                   aes_blocks_per_s=aes * c.world / sec)
-    # The dominant kernel is the tree (LDS-bound); the two phases are timed
-    # apart below, and the top-level roofline is the tree's own.
+    # Which kernel shape the step ran: the fused tree + fold launch
+    # (k_pir_fused, dpf_pir_kernel_for) or the tree launch then the fold
+    # launch.  The two phases of the two-launch path are timed apart below
+    # either way (pir_breakdown).
+    fused = a.pir_fold == "mfma" and dpf.pir_kernel_for(nk, logN, pb) == dpf.PIR_FUSED
     kern = pir_breakdown(c, W, d_db, lo, hi, nk, min(a.steps, 20))
     line["kernels"] = kern
-    line["roofline"] = prg_roofline(aes / (kern["tree"]["kernel_ms"] * 1e-3), "k_evalfull (PIR tree)",
-                                    kern["tree"]["kernel_ms"], nk * ((hi - lo) // 8), workload="pir",
-                                    profiled_shape=(W == 1 and nk == 64))
+    line["pir_kernel"] = "fused" if fused else "split"
+    if fused:
+        # One launch holds both phases: the roofline is the LDS-bound AES of
+        # the tree (lookups/s over the step's kernels: unpack + k_pir_fused +
+        # k_xor_parts), and the DB stream it folds on the matrix cores rides
+        # under it (its HBM rate beside it, not the bound).
+        line["roofline"] = prg_roofline(aes / (k_ms * 1e-3), "k_pir_fused (tree + MFMA fold)", k_ms,
+                                        (hi - lo) * 32, workload="pir_fused",
+                                        profiled_shape=(W == 1 and nk == 64))
+        db_gbs = (hi - lo) * 32 / (k_ms * 1e-3) / 1e9
+        line["roofline"]["fold"] = {"bound": "hbm (not binding: under the tree in the same launch)",
+                                    "achieved": round(db_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": round(db_gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": (hi - lo) * 32,
+                                    "note": "DB slice read once per batch; the selection bits stay in LDS"}
+        line["roofline"]["split_path_ms"] = round(kern["tree"]["kernel_ms"] + kern["fold"]["kernel_ms"], 4)
+    else:
+        line["roofline"] = prg_roofline(aes / (kern["tree"]["kernel_ms"] * 1e-3), "k_evalfull (PIR tree)",
+                                        kern["tree"]["kernel_ms"], nk * ((hi - lo) // 8), workload="pir",
+                                        profiled_shape=(W == 1 and nk == 64))
+        line["roofline"]["fold"] = kern["fold"]["roofline"]
     line["roofline"]["step_kernel_ms"] = round(k_ms, 4)
-    line["roofline"]["fold"] = kern["fold"]["roofline"]
     line["pir_db"] = c.pir_layout
     if c.world == 1 and not a.no_sweep:
         # B in {1, 16, 64, 256}; the fold reads the DB once per

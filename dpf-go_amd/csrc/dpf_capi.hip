@@ -1024,6 +1024,33 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     return DPF_OK;
 }
 
+// PIR kernel over the sliced DB: the tree launch then the fold launch
+// (DPF_PIR_SPLIT, the default: measured faster), or both in one launch
+// where it applies (DPF_PIR_FUSED, k_pir_fused).  DPF_PIR_KERNEL=split|
+// fused|fused-any sets the start value.
+std::atomic<int> g_pir_kernel{[] {
+    const char* e = getenv("DPF_PIR_KERNEL");
+    if (e && strcmp(e, "fused-any") == 0) return DPF_PIR_FUSED_ANY;
+    if (e && e[0] == 'f') return DPF_PIR_FUSED;
+    return DPF_PIR_SPLIT;
+}()};
+
+int dpf_set_pir_kernel(int kernel) {
+    if (kernel != DPF_PIR_SPLIT && kernel != DPF_PIR_FUSED && kernel != DPF_PIR_FUSED_ANY)
+        return fail(DPF_ERR_PARAM, "dpf: unknown PIR kernel");
+    return g_pir_kernel.exchange(kernel);
+}
+int dpf_get_pir_kernel(void) { return g_pir_kernel.load(); }
+
+int dpf_pir_kernel_for(size_t nkeys, uint32_t logN, uint32_t prefix_bits) {
+    const uint32_t stop = stop_of(logN);
+    const int k = g_pir_kernel.load(std::memory_order_relaxed);
+    return !want_bs() && k != DPF_PIR_SPLIT && prefix_bits <= stop &&
+                   dpfk::pir_fused_ok(nkeys, stop, prefix_bits, k == DPF_PIR_FUSED_ANY)
+               ? DPF_PIR_FUSED
+               : DPF_PIR_SPLIT;
+}
+
 size_t dpf_pir_db_sliced_size(uint64_t nrec) { return std::max<size_t>(16, dpfk::pir_sliced_bytes(nrec)); }
 
 int dpf_pir_db_slice_dev(int device, const uint8_t* d_db, uint64_t nrec, uint8_t* d_dbs, void* stream) {
@@ -1054,6 +1081,18 @@ int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t klen, si
     uint8_t* bits = (uint8_t*)d_work + align256(tree_ws_bytes(nkeys, stop, prefix_bits, nkeys));
     const uint64_t per_key = (uint64_t)16 << (stop - prefix_bits);
     const bool bs = want_bs();
+    const int fz = g_pir_kernel.load(std::memory_order_relaxed);
+    if (!bs && fz != DPF_PIR_SPLIT && dpfk::pir_fused_ok(nkeys, stop, prefix_bits, fz == DPF_PIR_FUSED_ANY)) {
+        // One launch: tree + matrix-core fold (k_pir_fused) from the expanded records.
+        const TreeWs w = tree_ws(d_work, nkeys, stop);
+        forget_expanded(d_work);
+        HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop, w.ek, st));
+        note_expanded(d_work, nkeys, stop, false);
+        uint32_t* parts = (uint32_t*)(bits + align256(nkeys * per_key));
+        HIP_TRY(dpfk::launch_pir_fused(w.ek, (uint32_t)nkeys, stop, prefix_bits, prefix, d_dbs, nrec, (uint32_t*)d_ans,
+                                       parts, st));
+        return DPF_OK;
+    }
     bool expanded = false;
     forget_expanded(d_work);
     HIP_TRY(tree_from_keys(d_keys, klen, nkeys, stop, prefix_bits, prefix, bits, per_key, d_work, st, bs, &expanded));

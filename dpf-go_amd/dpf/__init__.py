@@ -87,6 +87,9 @@ SIGNATURES = {
     "dpf_get_aes_impl": (_int, []),
     "dpf_set_eval_kernel": (_int, [_int]),
     "dpf_get_eval_kernel": (_int, []),
+    "dpf_set_pir_kernel": (_int, [_int]),
+    "dpf_get_pir_kernel": (_int, []),
+    "dpf_pir_kernel_for": (_int, [_sz, _u32, _u32]),
     "dpf_aes_mmo_dev": (_int, [_int, _int, _int, _vp, _vp, _sz, _u32, _vp]),
     "dpf_xor_fold_workspace_size": (_sz, []),
     "dpf_xor_fold_dev": (_int, [_int, _vp, _sz, _sz, _vp, _u64, _sz, _vp, _vp, _vp]),
@@ -401,6 +404,28 @@ def set_eval_kernel(kernel) -> int:
 
 def get_eval_kernel() -> int:
     return int(lib().dpf_get_eval_kernel())
+
+
+PIR_SPLIT, PIR_FUSED, PIR_FUSED_ANY = 0, 1, 2
+
+
+def set_pir_kernel(kernel) -> int:
+    """Select the sliced PIR kernel ("split"/"fused"/"fused-any" or 0/1/2); returns the previous one."""
+    if isinstance(kernel, str):
+        kernel = {"split": PIR_SPLIT, "fused": PIR_FUSED, "fused-any": PIR_FUSED_ANY}[kernel]
+    rc = lib().dpf_set_pir_kernel(kernel)
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+def get_pir_kernel() -> int:
+    return int(lib().dpf_get_pir_kernel())
+
+
+def pir_kernel_for(nkeys: int, logN: int, prefix_bits: int = 0) -> int:
+    """PIR_FUSED or PIR_SPLIT: what pir_answer_sliced_dev runs for this shape now."""
+    return int(lib().dpf_pir_kernel_for(nkeys, logN, prefix_bits))
 
 
 SMALL_AUTO, SMALL_GPU, SMALL_HOST = 0, 1, 2

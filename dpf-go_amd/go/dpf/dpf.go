@@ -229,3 +229,34 @@ func SetEvalKernel(kernel int) int {
 func GetEvalKernel() int {
 	return int(C.dpf_get_eval_kernel())
 }
+
+// PIR kernel of the sliced PIR path (include/dpf_hip.h DPF_PIR_*): PirSplit
+// (default) runs the tree launch then the fold launch, PirFused runs the
+// subtree EvalFull and the matrix-core fold in one launch where it applies
+// (<= 64 keys, logN - prefix_bits = 24..26; measured slower on MI355X),
+// PirFusedAny fuses from logN - prefix_bits = 16 (test mode).  Answers are
+// identical.  Returns the previous one.
+const (
+	PirSplit    = 0
+	PirFused    = 1
+	PirFusedAny = 2
+)
+
+func SetPirKernel(kernel int) int {
+	rc := C.dpf_set_pir_kernel(C.int(kernel))
+	if rc < 0 {
+		check(rc)
+	}
+	return int(rc)
+}
+
+// GetPirKernel returns the current PIR kernel setting (dpf_get_pir_kernel).
+func GetPirKernel() int {
+	return int(C.dpf_get_pir_kernel())
+}
+
+// PirKernelFor reports which kernel a PIR answer of this shape runs now
+// (dpf_pir_kernel_for): PirFused or PirSplit.
+func PirKernelFor(nkeys int, logN uint64, prefixBits uint32) int {
+	return int(C.dpf_pir_kernel_for(C.size_t(nkeys), C.uint32_t(logN), C.uint32_t(prefixBits)))
+}

@@ -248,6 +248,25 @@ int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t key_len,
                               uint8_t* d_ans, void* d_work, void* stream);
 int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_dbs,
                             uint64_t nrec, uint8_t* d_ans, void* d_work, void* stream);
+/* Kernel shape of dpf_pir_answer_sliced_dev (and of a sliced PIR handle):
+ * DPF_PIR_SPLIT (default): a tree launch writes the selection bits to HBM
+ * and a fold launch reads them back.  DPF_PIR_FUSED: where nkeys <= 64 and
+ * the slice holds 2^8..2^10 blocks of 256 leaf pairs (logN - prefix_bits =
+ * 24..26), one launch runs the subtree EvalFull and the matrix-core fold
+ * together (k_pir_fused: per CU, 12 waves expand the tree with one key per
+ * lane and 4 waves fold each leaf pair from LDS), so the selection bits
+ * never reach HBM; measured slower on MI355X, the split
+ * path elsewhere.  DPF_PIR_FUSED_ANY fuses any slice from logN -
+ * prefix_bits = 16 (test mode).  Answers are identical.  Process-wide; env
+ * DPF_PIR_KERNEL=split|fused|fused-any. */
+#define DPF_PIR_SPLIT 0
+#define DPF_PIR_FUSED 1
+#define DPF_PIR_FUSED_ANY 2
+int dpf_set_pir_kernel(int kernel);   /* returns the previous kernel */
+int dpf_get_pir_kernel(void);
+/* What dpf_pir_answer_sliced_dev runs for this shape under the current
+ * setting and AES back end: DPF_PIR_FUSED or DPF_PIR_SPLIT. */
+int dpf_pir_kernel_for(size_t nkeys, uint32_t logN, uint32_t prefix_bits);
 
 /* Host form: the DB is uploaded once, sharded by top-level subtree over
  * ngpus devices (a power of two), each GPU folds its slice and the host
