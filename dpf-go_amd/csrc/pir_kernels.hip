@@ -126,6 +126,12 @@ __device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool liv
 #ifndef DPF_FZ_BATCH
 #define DPF_FZ_BATCH 0        // k_pir_fused producers: batched AES rounds (aes2_rounds<BATCH>)
 #endif
+#ifndef DPF_FZ_NOFOLD
+#define DPF_FZ_NOFOLD 0       // measurement only: folders take the ring entries without folding them
+#endif
+#ifndef DPF_FZ_TOUCH
+#define DPF_FZ_TOUCH 1        // k_pir_fused producers touch the next super-group into L2
+#endif
 #ifndef DPF_FOLD_PRIO
 #define DPF_FOLD_PRIO 1   // issue priority by progress (fold_prio)
 #endif
@@ -1084,66 +1090,45 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
 
 // ---------------------------------------------------------------------------
 // Fused PIR answer: the subtree EvalFull and the matrix-core fold in ONE
-// launch, so the selection bits never reach HBM.
+// launch, so the fold's MFMA and HBM streams run under the tree's LDS-bound
+// AES instead of after it.  The selection bits never reach
+// HBM.
 //
 // One 1024-thread workgroup (16 waves, the whole CU: one 64 KiB T-table)
 // per block of 256 leaf pairs of the subtree, i.e. 256 super-groups (65,536
-// records) of the DB, for up to 64 keys.  Every wave is a producer AND a
-// folder:
-//   - lane = key.  Wave w evaluates the 16 pairs [16w, 16w + 16) of the
-//     block, an aligned subtree 4 levels below the block root, for all keys,
-//     depth-first as evalFullRecursive does (dpf/dpf.go:213-241).  A leaf
-//     pair is the two leaves under a node at level stop - 1: 32 bytes = 256
-//     selection bits = one super-group of the sliced DB.  Pair i of every
-//     wave goes to ring slot i & 1 in LDS ("period" i).
-//   - after emitting pair i, wave w folds period i - 1 for its answer tile
-//     (keys 32 (w & 1) .. +31, answer bits 32 (w >> 1) .. +31): the 16 pairs
-//     of that period = 64 v_mfma_scale_f32_32x32x64_f8f6f4 as k_fold_mfma
-//     does, selection words from the ring (ds_read_b128), DB words from the
-//     sliced DB (the producer touched its next super-group into L2 a period
-//     earlier).  Counts <= 4096 per period are exact; their parities are
-//     XORed into one register per wave, so no accumulator lives across the
-//     tree work.
-// Waves are ordered by per-period LDS counters, not barriers (a barrier per
-// pair made every wave wait for the period's slowest, profiles/r04/fused):
-// a wave folds period i - 1 once all 16 waves have written it, and writes
-// slot i & 1 once all 16 have folded period i - 2.  Every wait is bounded.
-// Measured (profiles/r04/fused/summary.txt): the first design -- 12
-// producer waves + 4 folder waves -- ran at 0.45-0.47 ms per configs[4]
-// step against 0.41 for the two-launch path: 3 key-per-lane producer waves
-// per SIMD needed 0.39 ms for the tree alone (16 waves: 0.30).
-constexpr int kFzWaves = 16;
-constexpr int kFzThreads = 64 * kFzWaves;
+// records) of the DB, for up to 64 keys:
+//   waves 0..11  producers: lane = key.  Wave p evaluates pairs [a0, a1) of
+//                the block (21-22 of them) for all keys, depth-first as
+//                evalFullRecursive does (dpf/dpf.go:213-241): a leaf pair is
+//                the two leaves under a node at level stop-1, 32 bytes = 256
+//                selection bits = one super-group of the sliced DB.  Each
+//                pair goes to a ring slot in LDS, then a workgroup barrier.
+//   waves 12..15 folders (one per SIMD): after the barrier of period t, the
+//                12 pairs of period t are folded by v_mfma_scale_f32_32x32x64
+//                _f8f6f4 exactly as k_fold_mfma does: folder f owns answer
+//                bits 64f..64f+63 of every key (2 x 2 tiles, 64 accumulator
+//                registers), selection words from the ring (ds_read_b128),
+//                DB words from the sliced DB in HBM.
+// The ring has two slots: a slot is refilled two periods later, after the
+// folders passed the barrier that ends their fold of it, so one barrier per
+// period orders both directions.  A producer walks from the block root
+// (walked once for all keys by folder wave 0 at the start, in LDS) 3 levels
+// down to each 32-pair piece of its range and expands only the nodes over
+// its pairs (fz_visit: one AES where the range leaves one child).
+#ifndef DPF_FZ_PRODONLY
+#define DPF_FZ_PRODONLY 0     // measurement only: 16 producer waves, no folders, no ring flow control
+#endif
+constexpr int kFzProd = DPF_FZ_PRODONLY ? 16 : 12;   // producer waves
+constexpr int kFzFold = DPF_FZ_PRODONLY ? 0 : 4;     // folder waves
+constexpr int kFzThreads = 64 * (kFzProd + kFzFold);
 constexpr uint32_t kFzBlockPairs = 256;      // leaf pairs (= DB super-groups) per workgroup
 constexpr uint32_t kFzBlockLog = 8;
-constexpr uint32_t kFzSubLog = 4;            // a wave's pairs: the subtree 4 levels below the block root
-constexpr uint32_t kFzPairs = 1u << kFzSubLog;
-constexpr uint32_t kFzSlot = kFzWaves * 64 * 8;   // words per ring slot: [wave][key][8], 16-B halves swizzled
-constexpr uint32_t kFzSpin = 1u << 22;
+constexpr uint32_t kFzSubLog = 5;            // a walked piece: 32 pairs below a node 5 levels up
+constexpr uint32_t kFzRow = 12;              // words per key row of a slot (8 + 4: conflict-free b128 reads)
+constexpr uint32_t kFzSlot = kFzProd * 64 * kFzRow;
+constexpr uint32_t kFzPeriods = (kFzBlockPairs + kFzProd - 1) / kFzProd;   // 22
 
-__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Per-period counters in LDS: s_pcnt[i] = waves that wrote their pair i,
-// s_fcnt[i] = waves that folded period i.  A wave waits (bounded) until a
-// counter reaches kFzWaves; lane 0 counts for its wave after a release
-// fence (the s_waitcnt of the release covers every lane's LDS writes).
-__device__ __forceinline__ void fz_wait(const uint32_t* cnt) {
-    for (uint32_t n = 0; n < kFzSpin && lds_acquire(cnt) < (uint32_t)kFzWaves; ++n) __builtin_amdgcn_s_sleep(1);
-}
-__device__ __forceinline__ void fz_count(uint32_t* cnt, uint32_t lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Word offset of half h (16 B) of key k's 32-byte row: halves swapped for
-// k & 8, so the 16 lanes of a ds_read_b128 / ds_write_b128 pass hit 64
-// distinct banks.
-__device__ __forceinline__ uint32_t fz_row(uint32_t w, uint32_t k, uint32_t h) {
-    return (w * 64 + k) * 8 + 4 * (h ^ ((k >> 3) & 1u));
-}
+__device__ __forceinline__ uint32_t fz_a0(uint32_t p) { return kFzBlockPairs * p / kFzProd; }
 
 struct FzCtx {
     const uint8_t* tab;
@@ -1151,65 +1136,30 @@ struct FzCtx {
     const uint32_t* ek;    // this lane's expanded key records (k_unpack)
     Blk fcw;
     uint32_t P;            // level of a leaf pair's parent: stop - 1
-    uint32_t w, l;         // wave, lane
+    uint32_t* row;         // this lane's row in ring slot 0 (slot 1 at + kFzSlot)
     uint32_t period;       // pairs emitted so far
     uint32_t live;         // ~0: lane < nkeys
-    uint32_t* ring;
-    uint32_t* pcnt;        // s_pcnt[i]: waves that wrote pair i
-    uint32_t* fcnt;        // s_fcnt[i]: waves that folded period i
-    const uint4* dbs;      // sliced DB
-    uint64_t sg0;          // super-group of this workgroup's pair 0
+    uint32_t p;            // producer index (wave)
+    uint32_t* prod;        // s_prod: pairs written, per producer
+    const uint32_t* fold;  // s_fold: ring entries folded, per folder
+    const uint32_t* dbw;   // sliced DB as words; the producer's next super-group is touched into L2
+    uint64_t sg;           // super-group of the pair being computed
     uint64_t nsg;
-    uint32_t touch;        // last L2 touch (consumed a pair later)
-    uint32_t par;          // answer bits of this wave's tile (lane < 32: row = key 32 (w & 1) + lane)
+    uint32_t touch;        // last touch load (consumed one pair later)
 };
 
-typedef int fz_v8i __attribute__((ext_vector_type(8)));
-typedef float fz_v16f __attribute__((ext_vector_type(16)));
-
-// Fold period q (16 pairs, one per wave) into this wave's tile.
-__device__ __forceinline__ void fz_fold(FzCtx& c, uint32_t q) {
-    const uint32_t r = c.l & 31, h = c.l >> 5;
-    const uint32_t m = c.w & 1, nt = c.w >> 1;
-    const uint32_t* slot = c.ring + (q & 1) * kFzSlot;
-    const uint32_t key = 32 * m + r;
-    fold_v16f acc;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-#pragma unroll
-    for (uint32_t e0 = 0; e0 < (uint32_t)kFzWaves; e0 += 2) {
-        uint4 A[2], B[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const uint32_t e = e0 + i;
-            const uint64_t S = c.sg0 + e * kFzPairs + q;
-            const bool ok = S < c.nsg;
-            const uint4 x = c.dbs[((ok ? S : 0) * 256 + 32 * nt + r) * 2 + h];
-            B[i] = ok ? x : make_uint4(0, 0, 0, 0);
-            A[i] = *reinterpret_cast<const uint4*>(slot + fz_row(e, key, h));
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int t4 = 0; t4 < 4; ++t4)
-                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fp4_w7(u4w(A[i], t4)), fp4_w5(u4w(B[i], t4)), acc,
-                                                                     kFoldFp4, kFoldFp4, 0, kE8M0One, 0, kE8M0One);
-    }
-    fz_count(c.fcnt + q, c.l);
-    // Parities -> row words (C/D layout: lane = column, register e = rows
-    // (e & 3) + 8 (e >> 2) + 4 h), XORed into the running answer bits.
-    uint32_t out = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        const uint64_t b = __builtin_amdgcn_ballot_w64((((uint32_t)acc[e]) & 1u) != 0);
-        const uint32_t row0 = (e & 3) + 8 * (e >> 2);
-        out = c.l == row0 ? (uint32_t)b : out;
-        out = c.l == row0 + 4 ? (uint32_t)(b >> 32) : out;
-    }
-    c.par ^= out;
+// Workgroup-scope flags in LDS (ASYNC ring).  Every wait is bounded, so each
+// wave reaches its exit even if a flag were never set.
+constexpr uint32_t kFzSpin = 1u << 22;
+__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // The pair under node n (level P): two leaves (dpf.go:214-224) = 256 bits.
+template <bool ASYNC>
 __device__ __forceinline__ void fz_emit(FzCtx& c, const Node& n) {
     const CW cw = load_cw(c.ek, c.P);
     Node L, R;
@@ -1218,34 +1168,53 @@ __device__ __forceinline__ void fz_emit(FzCtx& c, const Node& n) {
     mmo_pair<DPF_FZ_BATCH>(c.tab, c.lo, KeyFixed<false>{}, L.s, oL, KeyFixed<false>{}, R.s, oR);
     oL = leaf_fix(oL, L.t, c.fcw);
     oR = leaf_fix(oR, R.t, c.fcw);
+    const uint32_t m = c.live;
     const uint32_t i = c.period;
-    // Touch this wave's next super-group (8 KiB, one line per lane) so the
-    // folds of the next period find it in L2; the previous touch is consumed
-    // here, a pair after it was issued.
+    // Touch the next pair's 8 KiB of the sliced DB (one 128-byte line per
+    // lane) so the folders find it in L2 a period later; the value of the
+    // previous touch is consumed here, long after it landed.
+#if DPF_FZ_TOUCH
     asm volatile("" ::"v"(c.touch));
     {
-        const uint64_t s = c.sg0 + c.w * kFzPairs + i + 1;
-        c.touch = reinterpret_cast<const uint32_t*>(c.dbs)[(s < c.nsg ? s : c.nsg - 1) * 2048 + c.l * 32];
+        const uint64_t s = c.sg + 1 < c.nsg ? c.sg + 1 : c.nsg - 1;
+        c.touch = c.dbw[s * 2048 + (threadIdx.x & 63) * 32];
+        c.sg += 1;
     }
-    if (i >= 2) fz_wait(c.fcnt + i - 2);       // slot i & 1 free: period i - 2 folded by every wave
-    const uint32_t m = c.live;
-    uint32_t* s = c.ring + (i & 1) * kFzSlot;
-    *reinterpret_cast<uint4*>(s + fz_row(c.w, c.l, 0)) = make_uint4(oL.c0 & m, oL.c1 & m, oL.c2 & m, oL.c3 & m);
-    *reinterpret_cast<uint4*>(s + fz_row(c.w, c.l, 1)) = make_uint4(oR.c0 & m, oR.c1 & m, oR.c2 & m, oR.c3 & m);
-    fz_count(c.pcnt + i, c.l);
+#endif
+    if constexpr (ASYNC && !DPF_FZ_PRODONLY) {
+        // Slot i & 1 is free once every folder has folded this producer's
+        // pair i - 2 (ring entry (i - 2) * kFzProd + p in folding order).
+        if (i >= 2) {
+            const uint32_t need = (i - 2) * kFzProd + c.p + 1;
+            for (uint32_t n = 0; n < kFzSpin; ++n) {
+                uint32_t lo_ = lds_acquire(c.fold);
+#pragma unroll
+                for (int f = 1; f < kFzFold; ++f) {
+                    const uint32_t v = lds_acquire(c.fold + f);
+                    lo_ = v < lo_ ? v : lo_;
+                }
+                if (lo_ >= need) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    uint32_t* row = c.row + (DPF_FZ_PRODONLY ? 0 : (i & 1) * kFzSlot);
+    *reinterpret_cast<uint4*>(row) = make_uint4(oL.c0 & m, oL.c1 & m, oL.c2 & m, oL.c3 & m);
+    *reinterpret_cast<uint4*>(row + 4) = make_uint4(oR.c0 & m, oR.c1 & m, oR.c2 & m, oR.c3 & m);
+    if constexpr (ASYNC) {
+        lds_release(c.prod + c.p, i + 1);
+    } else {
+        __syncthreads();
+    }
     c.period = i + 1;
-    if (i >= 1) {
-        fz_wait(c.pcnt + i - 1);               // period i - 1 written by every wave
-        fz_fold(c, i - 1);
-    }
 }
 
 // Pairs [lo, hi) of the 2^K pairs below node n (level P - K), in order.
 // lo, hi are wave-uniform; a child outside the range is never computed.
-template <int K>
+template <int K, bool ASYNC>
 __device__ __forceinline__ void fz_visit(FzCtx& c, const Node& n, uint32_t lo, uint32_t hi) {
     if constexpr (K == 0) {
-        fz_emit(c, n);
+        fz_emit<ASYNC>(c, n);
     } else {
         constexpr uint32_t half = 1u << (K - 1);
         const CW cw = load_cw(c.ek, c.P - K);
@@ -1265,25 +1234,24 @@ __device__ __forceinline__ void fz_visit(FzCtx& c, const Node& n, uint32_t lo, u
         for (uint32_t s = s0; s < s1; ++s) {
             const uint32_t clo = s == 0 ? lo : (lo > half ? lo - half : 0u);
             const uint32_t chi = s == 0 ? (hi < half ? hi : half) : hi - half;
-            fz_visit<K - 1>(c, ch, clo, chi);
+            fz_visit<K - 1, ASYNC>(c, ch, clo, chi);
             ch = pend;
         }
     }
 }
 
+template <bool ASYNC>
 __global__ __launch_bounds__(kFzThreads, 1) void k_pir_fused(const uint32_t* __restrict__ ek, uint32_t nkeys,
                                                             uint32_t stop, uint32_t pb, uint64_t prefix,
                                                             const uint4* __restrict__ dbs, uint64_t nsg,
                                                             uint32_t* __restrict__ parts, uint32_t* __restrict__ zero,
                                                             uint64_t zero_words) {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-    __shared__ __attribute__((aligned(16))) uint32_t s_ring[2 * kFzSlot];
+    __shared__ __attribute__((aligned(16))) uint32_t s_ring[(DPF_FZ_PRODONLY ? 1 : 2) * kFzSlot];
     __shared__ uint32_t s_top[64 * 5];
-    __shared__ uint32_t s_pcnt[kFzPairs], s_fcnt[kFzPairs];
-    if (threadIdx.x < kFzPairs) {
-        s_pcnt[threadIdx.x] = 0;
-        s_fcnt[threadIdx.x] = 0;
-    }
+    __shared__ uint32_t s_prod[kFzProd], s_fold[4];
+    if (threadIdx.x < kFzProd) s_prod[threadIdx.x] = 0;
+    if (threadIdx.x < 4) s_fold[threadIdx.x] = 0;
     zero_answers(zero, zero_words);
     fill_table(s_tab);
     const uint32_t l = threadIdx.x & 63;
@@ -1293,7 +1261,7 @@ __global__ __launch_bounds__(kFzThreads, 1) void k_pir_fused(const uint32_t* __r
     const uint32_t P = stop - 1;
     const uint32_t lb = P - kFzBlockLog;                      // level of the block root
     const uint32_t* kek = ek + (uint64_t)(l < nkeys ? l : 0) * ((uint64_t)(stop + 2) * 8);
-    if (wv == 0) {
+    if (wv == (DPF_FZ_PRODONLY ? 0 : kFzProd)) {
         // Block root of every key: prefix bits, then the block index (dpf.go:183-201 path).
         const uint64_t path = (prefix << (lb - pb)) | blockIdx.x;
         Node n;
@@ -1305,36 +1273,135 @@ __global__ __launch_bounds__(kFzThreads, 1) void k_pir_fused(const uint32_t* __r
         f[0] = n.s.c0; f[1] = n.s.c1; f[2] = n.s.c2; f[3] = n.s.c3; f[4] = n.t;
     }
     __syncthreads();
-    FzCtx c;
-    c.tab = tab;
-    c.lo = lo;
-    c.ek = kek;
-    c.fcw = load_blk(kek + 8 + 8 * stop);
-    c.P = P;
-    c.w = wv;
-    c.l = l;
-    c.period = 0;
-    c.live = l < nkeys ? ~0u : 0u;
-    c.ring = s_ring;
-    c.pcnt = s_pcnt;
-    c.fcnt = s_fcnt;
-    c.dbs = dbs;
-    c.sg0 = (uint64_t)blockIdx.x * kFzBlockPairs;
-    c.nsg = nsg;
-    c.touch = 0;
-    c.par = 0;
-    const uint32_t* f = s_top + 5 * l;
-    Node n;
-    n.s = {f[0], f[1], f[2], f[3]};
-    n.t = f[4];
+    if (wv < kFzProd) {
+        FzCtx c;
+        c.tab = tab;
+        c.lo = lo;
+        c.ek = kek;
+        c.fcw = load_blk(kek + 8 + 8 * stop);
+        c.P = P;
+        c.row = s_ring + (wv * 64 + l) * kFzRow;
+        c.period = 0;
+        c.live = l < nkeys ? ~0u : 0u;
+        c.p = wv;
+        c.prod = s_prod;
+        c.fold = s_fold;
+        c.dbw = reinterpret_cast<const uint32_t*>(dbs);
+        c.nsg = nsg;
+        c.touch = 0;
+        const uint32_t* f = s_top + 5 * l;
+        Node top;
+        top.s = {f[0], f[1], f[2], f[3]};
+        top.t = f[4];
+        const uint32_t a0 = fz_a0(wv), a1 = fz_a0(wv + 1);
+        for (uint32_t a = a0; a < a1;) {
+            const uint32_t j = a >> kFzSubLog;
+            const uint32_t b = (j + 1) << kFzSubLog < a1 ? (j + 1) << kFzSubLog : a1;
+            c.sg = (uint64_t)blockIdx.x * kFzBlockPairs + a;
+            Node n = top;
 #pragma nounroll
-    for (uint32_t i = 0; i < kFzBlockLog - kFzSubLog; ++i)       // block root -> this wave's subtree root
-        walk_step<false>(tab, lo, n, load_cw(kek, lb + i), (wv >> (kFzBlockLog - kFzSubLog - 1 - i)) & 1u);
-    fz_visit<kFzSubLog>(c, n, 0, kFzPairs);
-    fz_wait(s_pcnt + kFzPairs - 1);                                 // the last period
-    fz_fold(c, kFzPairs - 1);
-    asm volatile("" ::"v"(c.touch));
-    if (l < 32) parts[((uint64_t)blockIdx.x * 64 + 32 * (wv & 1) + l) * 8 + (wv >> 1)] = c.par;
+            for (uint32_t i = 0; i < kFzBlockLog - kFzSubLog; ++i)
+                walk_step<false>(tab, lo, n, load_cw(kek, lb + i), (j >> (kFzBlockLog - kFzSubLog - 1 - i)) & 1u);
+            fz_visit<kFzSubLog, ASYNC>(c, n, a - (j << kFzSubLog), b - (j << kFzSubLog));
+            a = b;
+        }
+        if constexpr (!ASYNC) {
+            while (c.period < kFzPeriods) {   // idle periods (21 of 22 pairs)
+                __syncthreads();
+                ++c.period;
+            }
+        }
+        return;
+    }
+    // Folders.
+    const uint32_t fw = wv - kFzProd, h = l >> 5, r = l & 31;
+    const uint64_t S0 = (uint64_t)blockIdx.x * kFzBlockPairs;
+    fold_v16f acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[m][j][e] = 0.0f;
+    // DB words of step q = (period t, producer p): dbs[S][64 fw + 32 j + r][4h .. 4h+3]
+    // for S = S0 + a0(p) + t; zero where p has no pair in t or S is past the DB.
+    auto ldb = [&](uint32_t q, uint4 (&B)[2]) __attribute__((always_inline)) {
+        const uint32_t t = q / kFzProd, p = q % kFzProd;
+        const uint32_t a = fz_a0(p) + t;
+        const uint64_t S = S0 + a;
+        const bool ok = a < fz_a0(p + 1) && S < nsg;
+        const uint64_t Sc = ok ? S : 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint4 x = dbs[(Sc * 256 + 64 * fw + 32 * j + r) * 2 + h];
+            B[j] = ok ? x : make_uint4(0, 0, 0, 0);
+        }
+    };
+    // Ring entries in folding order q = t * kFzProd + p.  The DB words of an
+    // entry are loaded two entries before it is folded, and its producer
+    // touched them a pair earlier (fz_emit), so they come from L2: one entry
+    // is ~0.2 us of MFMA work against ~1-2 us of HBM latency, and with the
+    // words fetched from HBM one entry ahead the folders, not the producers,
+    // set the kernel time (0.45 vs 0.41 ms for the two-launch path).
+    constexpr uint32_t Q = kFzPeriods * kFzProd;
+    static_assert(Q % 2 == 0, "two DB buffers in rotation");
+    auto fold_entry = [&](uint32_t q, const uint4 (&B)[2]) __attribute__((always_inline)) {
+        const uint32_t t = q / kFzProd, p = q % kFzProd;
+        if constexpr (!ASYNC) {
+            if (p == 0) __syncthreads();                        // period t's pairs are in slot t & 1
+        }
+        const bool has = fz_a0(p) + t < fz_a0(p + 1);           // producer p has a pair t (uniform)
+        if constexpr (ASYNC) {
+            if (has)
+                for (uint32_t n = 0; n < kFzSpin && lds_acquire(s_prod + p) <= t; ++n) __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t* rows = s_ring + (t & 1) * kFzSlot + p * 64 * kFzRow;
+        uint4 A[2];   // stale when !has: the DB words are zero then (e2m1 has no NaN/Inf)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) A[m] = *reinterpret_cast<const uint4*>(rows + (32 * m + r) * kFzRow + 4 * h);
+        if constexpr (ASYNC) lds_release(s_fold + fw, q + 1);  // after the reads: the slot may be refilled
+        if (DPF_FZ_NOFOLD) return;
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4) {
+            fold_v8i bo[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bo[j] = fp4_w5(u4w(B[j], t4));
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const fold_v8i ao = fp4_w7(u4w(A[m], t4));
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ao, bo[j], acc[m][j], kFoldFp4, kFoldFp4,
+                                                                               0, kE8M0One, 0, kE8M0One);
+            }
+        }
+    };
+    auto nxt = [&](uint32_t q) { return q < Q ? q : Q - 1; };
+    uint4 B0[2], B1[2];
+    ldb(0, B0);
+    ldb(1, B1);
+    for (uint32_t q = 0; q < Q; q += 2) {
+        fold_entry(q, B0);
+        ldb(nxt(q + 2), B0);
+        fold_entry(q + 1, B1);
+        ldb(nxt(q + 3), B1);
+    }
+    // Parities -> parts[block][key][8]: folder fw holds answer words 2 fw + j.
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            uint32_t out = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const uint32_t pbit = ((uint32_t)acc[m][j][e]) & 1u;
+                const uint64_t b = __builtin_amdgcn_ballot_w64(pbit != 0);
+                const uint32_t row0 = (e & 3) + 8 * (e >> 2);
+                out = l == row0 ? (uint32_t)b : out;
+                out = l == row0 + 4 ? (uint32_t)(b >> 32) : out;
+            }
+            if (l < 32) parts[((uint64_t)blockIdx.x * 64 + 32 * m + l) * 8 + 2 * fw + j] = out;
+        }
 }
 
 bool pir_fused_ok(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits, bool any_size) {
@@ -1349,8 +1416,18 @@ hipError_t launch_pir_fused(const uint32_t* ek, uint32_t nkeys, uint32_t stop, u
     if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * 32, st);
     const uint64_t nsg = (nrec + 255) / 256;
     const uint32_t blocks = 1u << (stop - 1 - kFzBlockLog - prefix_bits);
-    hipLaunchKernelGGL(k_pir_fused, dim3(blocks), dim3(kFzThreads), 0, st, ek, nkeys, stop, prefix_bits, prefix,
-                       reinterpret_cast<const uint4*>(dbs), nsg, parts, ans, (uint64_t)nkeys * 8);
+    // DPF_PIR_FUSED_SYNC=1: producers and folders in lockstep (one workgroup
+    // barrier per pair) instead of per-producer LDS flags (A/B runs).
+    static const bool sync = [] {
+        const char* e = getenv("DPF_PIR_FUSED_SYNC");
+        return e && e[0] == '1';
+    }();
+    if (sync)
+        hipLaunchKernelGGL(k_pir_fused<false>, dim3(blocks), dim3(kFzThreads), 0, st, ek, nkeys, stop, prefix_bits,
+                           prefix, reinterpret_cast<const uint4*>(dbs), nsg, parts, ans, (uint64_t)nkeys * 8);
+    else
+        hipLaunchKernelGGL(k_pir_fused<true>, dim3(blocks), dim3(kFzThreads), 0, st, ek, nkeys, stop, prefix_bits,
+                           prefix, reinterpret_cast<const uint4*>(dbs), nsg, parts, ans, (uint64_t)nkeys * 8);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     const uint32_t ys = blocks < 64 ? blocks : 64;
     hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * 8 + 255) / 256, ys), dim3(256), 0, st, parts, (uint64_t)blocks, nkeys,
