@@ -1,7 +1,7 @@
 #!/bin/bash
 # Fused PIR kernel (k_pir_fused): parity tests, then the PIR bench line with
-# the two-launch kernel and the fused kernel, interleaved; then a kernel
-# trace of both.  Output: gpurun_out/fz/ ($1: sub-directory).
+# the two-launch kernel and the fused kernel, interleaved.
+# Output: gpurun_out/fz/$1/.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/fz/${1:-run}
@@ -12,4 +12,3 @@ for i in 1 2; do
   DPF_PIR_KERNEL=split timeout -k 10 200 python bench.py --workload pir --steps 100 --warmup 10 --no-cpu-baseline --no-sweep --check > $O/pir_split_$i.log 2>&1 || exit $?
   DPF_PIR_KERNEL=fused timeout -k 10 200 python bench.py --workload pir --steps 100 --warmup 10 --no-cpu-baseline --no-sweep --check > $O/pir_fused_$i.log 2>&1 || exit $?
 done
-DPF_PIR_KERNEL=fused timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt -- python3 bench.py --workload pir --steps 50 --warmup 5 --no-cpu-baseline --no-sweep > $O/kt.log 2>&1 || exit $?
