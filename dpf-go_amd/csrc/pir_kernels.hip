@@ -1090,9 +1090,13 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
 
 // ---------------------------------------------------------------------------
 // Fused PIR answer: the subtree EvalFull and the matrix-core fold in ONE
-// launch, so the fold's MFMA and HBM streams run under the tree's LDS-bound
-// AES instead of after it.  The selection bits never reach
-// HBM.
+// launch, so the fold's MFMA and HBM streams could run under the tree's
+// LDS-bound AES instead of after it.  The selection bits
+// never reach HBM.  Bit-exact, and measured SLOWER than the two launches
+// (0.45-0.47 vs 0.41 ms per configs[4] step, profiles/r04/fused/): one key
+// per lane and 3 producer waves per SIMD need 0.39 ms for the tree alone,
+// against 0.25 ms for the one-key-per-wave kernel at 4 waves per SIMD.  So
+// it is opt-in (dpf_set_pir_kernel(DPF_PIR_FUSED)).
 //
 // One 1024-thread workgroup (16 waves, the whole CU: one 64 KiB T-table)
 // per block of 256 leaf pairs of the subtree, i.e. 256 super-groups (65,536
