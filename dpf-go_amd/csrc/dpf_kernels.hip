@@ -490,6 +490,9 @@ __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekey
 #ifndef DPF_EVAL_EARLY
 #define DPF_EVAL_EARLY 1
 #endif
+#ifndef DPF_EVAL_PREFETCH
+#define DPF_EVAL_PREFETCH 0   // strided k_eval2: next pair's inputs requested before the current walk (A/B)
+#endif
 __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                      uint32_t logN, const uint64_t* __restrict__ xs, uint64_t nq,
                                                      uint64_t pts_per_key, const uint4* __restrict__ fseed,
@@ -520,6 +523,21 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
 #else
     const uint64_t it0 = 0;
 #endif
+#if DPF_EVAL_PREFETCH
+    // Strided form with the next pair's points and frontier nodes requested
+    // before the current pair's walk, so their HBM latency hides under it.
+    PairIn nx{};
+    if (it0 < iters) nx = eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, first + it0 * stride);
+    for (uint64_t it = it0; it < iters; ++it) {
+        if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
+        else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
+        else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
+        const uint64_t q0 = first + it * stride;
+        const PairIn cur = nx;
+        if (it + 1 < iters) nx = eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0 + stride);
+        eval_pair_walk(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, q0, cur);
+    }
+#else
     for (uint64_t it = it0; it < iters; ++it) {
         if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
@@ -528,6 +546,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
         eval_pair_walk(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, q0,
                        eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0));
     }
+#endif
 }
 
 // Batched Eval as a visited-node trie below the frontier.
