@@ -74,7 +74,7 @@ struct Ctx {
 // the ones behind and a SIMD's waves finish close together (busy 95%;
 // kernel 1048 -> 948 us on one box, profiles/r03/prio/).
 //   DPF_PRIO_STEPS 3: thresholds 3/4, 7/8, 15/16 (default);
-//   2: 1/2, 3/4, 7/8;  1: 1/4, 1/2, 3/4;  0: off.
+//   2: 1/2, 3/4, 7/8;  1: 1/4, 1/2, 3/4;  5: 7/8, 15/16, 31/32;  0: off.
 //   Subtrees of <= 2^5 leaf blocks (8 or fewer groups: the PIR tree, strong-
 //   scaling ranks) step at 1/2, 3/4, 7/8 (DPF_PRIO_STEPS_SMALL 2): at the
 //   PIR shape waves are busy 0.945-0.949 of the span instead of 0.914-0.922
@@ -88,10 +88,10 @@ __device__ __forceinline__ void prio_step(Ctx& c) {
     constexpr int S = DMAX <= 5 ? DPF_PRIO_STEPS_SMALL : DPF_PRIO_STEPS;
     constexpr uint32_t total = DMAX >= 2 ? 1u << (DMAX - 2) : 1u;   // 4-leaf groups per thread
     const uint32_t d = ++c.groups;
-    constexpr uint32_t den = S == 1 ? 4 : S == 2 ? 8 : 16;
-    constexpr uint32_t t1 = S == 1 ? 1 : S == 2 ? 4 : 12;
-    constexpr uint32_t t2 = S == 1 ? 2 : S == 2 ? 6 : 14;
-    constexpr uint32_t t3 = S == 1 ? 3 : S == 2 ? 7 : 15;
+    constexpr uint32_t den = S == 1 ? 4 : S == 2 ? 8 : S == 5 ? 32 : 16;
+    constexpr uint32_t t1 = S == 1 ? 1 : S == 2 ? 4 : S == 5 ? 28 : 12;
+    constexpr uint32_t t2 = S == 1 ? 2 : S == 2 ? 6 : S == 5 ? 30 : 14;
+    constexpr uint32_t t3 = S == 1 ? 3 : S == 2 ? 7 : S == 5 ? 31 : 15;
     const uint32_t x = d * den;
     if (x >= t3 * total) __builtin_amdgcn_s_setprio(0);
     else if (x >= t2 * total) __builtin_amdgcn_s_setprio(1);
