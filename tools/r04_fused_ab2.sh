@@ -2,6 +2,9 @@
 # k_pir_fused producer rate with 16 producer waves (4 per SIMD), no folders
 # (DPF_FZ_PRODONLY; answers not meaningful), plain and batched AES rounds,
 # against the 12-producer no-fold variant.  gpurun_out/fz/ab2/.
+# The DPF_FZ_PRODONLY switch (kFzProd = 16, kFzFold = 0, one ring slot, no
+# flow control) was a measurement-only edit of the v3 kernel and was not
+# committed; the results are in profiles/r04/fused/ab2_*.json.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/fz/${1:-ab2}
