@@ -988,6 +988,18 @@ int dpf_evalfull_expanded_dev(int device, void* d_work, size_t nkeys, uint32_t l
 
 // ------------------------------------------------------------------ PIR ---
 
+// Device buffers of the PIR answer entry points: present when there is work
+// for them, and aligned as the kernels access them (DB 16 B, answers and
+// workspace as u32 words), so a bad buffer is DPF_ERR_PARAM, not a GPU fault.
+static int check_pir_bufs(const void* d_keys, size_t nkeys, const void* d_db, uint64_t nrec, const void* d_ans,
+                          const void* d_work) {
+    if (nkeys > 0 && (!d_keys || !d_ans || !d_work || (nrec > 0 && !d_db)))
+        return fail(DPF_ERR_PARAM, "dpf: null device buffer");
+    if ((uintptr_t)d_db % 16 != 0 || (uintptr_t)d_ans % 4 != 0 || (uintptr_t)d_work % 16 != 0)
+        return fail(DPF_ERR_PARAM, "dpf: misaligned device buffer");
+    return DPF_OK;
+}
+
 size_t dpf_pir_workspace_size(size_t nkeys, uint32_t logN, uint32_t prefix_bits) {
     const uint32_t stop = stop_of(logN);
     const uint32_t pb = prefix_bits > stop ? stop : prefix_bits;
@@ -1003,6 +1015,7 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     if (prefix_bits > stop || (prefix >> prefix_bits) != 0) return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
     const uint64_t slice = logN - prefix_bits >= 64 ? ~0ull : (1ull << (logN - prefix_bits));
     if (nrec > slice) return fail(DPF_ERR_PARAM, "dpf: more DB records than the subtree's domain");
+    if (int rc = check_pir_bufs(d_keys, nkeys, d_db, nrec, d_ans, d_work)) return rc;
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)stream;
     if (nkeys == 0) return DPF_OK;
@@ -1038,6 +1051,8 @@ std::atomic<int> g_pir_kernel{[] {
 int dpf_set_pir_kernel(int kernel) {
     if (kernel != DPF_PIR_SPLIT && kernel != DPF_PIR_FUSED && kernel != DPF_PIR_FUSED_ANY)
         return fail(DPF_ERR_PARAM, "dpf: unknown PIR kernel");
+    if (kernel != DPF_PIR_SPLIT && !dpfk::pir_fused_ok(1, 17, 0, true))
+        return fail(DPF_ERR_PARAM, "dpf: the fused PIR kernel is not in this build (make -C dpf-go_amd experimental)");
     return g_pir_kernel.exchange(kernel);
 }
 int dpf_get_pir_kernel(void) { return g_pir_kernel.load(); }
@@ -1069,7 +1084,7 @@ int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t klen, si
     if (prefix_bits > stop || (prefix >> prefix_bits) != 0) return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
     const uint64_t slice = logN - prefix_bits >= 64 ? ~0ull : (1ull << (logN - prefix_bits));
     if (nrec > slice) return fail(DPF_ERR_PARAM, "dpf: more DB records than the subtree's domain");
-    if ((uintptr_t)d_dbs % 16 != 0) return fail(DPF_ERR_PARAM, "dpf: misaligned device buffer");
+    if (int rc = check_pir_bufs(d_keys, nkeys, d_dbs, nrec, d_ans, d_work)) return rc;
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)stream;
     if (nkeys == 0) return DPF_OK;
@@ -1119,6 +1134,11 @@ int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_strid
 }
 
 size_t dpf_xor_fold_workspace_size(void) { return dpfk::pir_fold_parts_bytes(); }
+
+int dpf_set_fold_limits(uint32_t max_blocks, uint32_t parity_every) {
+    dpfk::set_fold_limits(max_blocks, parity_every);
+    return DPF_OK;
+}
 
 int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_payload,
                      uint64_t nrec, size_t rec_bytes, uint8_t* d_ans, void* d_work, void* stream) {

@@ -31,6 +31,7 @@
 //                  looked up by up to 4 x 64 keys (lane = key): 2
 //                  ds_read_b128 per key per group instead of 32 masked XORs.
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -519,14 +520,26 @@ static int cu_count_fold() {
 
 constexpr uint64_t kFoldMaxBlocks = 1024;          // workgroups per launch (partials area)
 constexpr uint64_t kFoldPartBytes = 64 * 4 * 32 * 2;   // largest part: 64*KW keys x 32C bytes, KW*C <= 8
+constexpr uint32_t kFoldParEveryMax = 1u << 15;    // k_fold_mfma: super-groups between parity reductions
 
 uint64_t pir_fold_parts_bytes() { return kFoldMaxBlocks * kFoldPartBytes; }
+
+// Tuning / test limits (set_fold_limits): workgroups per fold launch and the
+// MFMA fold's parity-reduction period.
+static std::atomic<uint32_t> g_fold_blocks{(uint32_t)kFoldMaxBlocks};
+static std::atomic<uint32_t> g_fold_par_every{kFoldParEveryMax};
+static uint32_t fold_par_every() { return g_fold_par_every.load(std::memory_order_relaxed); }
+void set_fold_limits(uint32_t max_blocks, uint32_t par_every) {
+    g_fold_blocks.store(max_blocks == 0 || max_blocks > kFoldMaxBlocks ? (uint32_t)kFoldMaxBlocks : max_blocks);
+    g_fold_par_every.store(par_every == 0 || par_every > kFoldParEveryMax ? kFoldParEveryMax : par_every);
+}
 
 namespace {
 
 // Split nchunks into `blocks` contiguous ranges of whole `gran`-chunk batches.
 void split_chunks(uint64_t nchunks, uint64_t want_blocks, uint64_t gran, uint64_t& blocks, uint64_t& cpb) {
-    if (want_blocks > kFoldMaxBlocks) want_blocks = kFoldMaxBlocks;
+    const uint64_t cap = g_fold_blocks.load(std::memory_order_relaxed);
+    if (want_blocks > cap) want_blocks = cap;
     cpb = (nchunks + want_blocks - 1) / want_blocks;
     cpb = (cpb + gran - 1) / gran * gran;
     blocks = (nchunks + cpb - 1) / cpb;
@@ -720,11 +733,18 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 // sel[S / G][sgm_keys][G * 8 words] (G = sgm_g: 1, or 4 = one 128-byte line
 // of a key per chunk, as the PIR tree kernel writes them), so a staged block
 // is one contiguous region instead of EvalFull's key-major [key][wpk words].
+// Exactness of the fp32 counts: an accumulator gains at most 64 per MFMA
+// (one per record of a K-block), and fp32 holds every integer up to 2^24.  A
+// wave's run of super-groups is unbounded (sg_per_block grows with the DB and
+// shrinks with the CU count), so every `par_every` super-groups (<=
+// kFoldParEveryMax = 2^15, i.e. 2^23 records) the accumulators are reduced to
+// their parities: count - 2 floor(count / 2), exact below 2^24.  Between two
+// reductions a count stays below (2^15 + 3 SG) * 256 < 2^24.
 template <int MT, int NT, int SG, int KG, int SGM = 0>
 __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
-    uint32_t sgm_keys = 0) {
+    uint32_t par_every, uint32_t sgm_keys = 0) {
     constexpr int NS = 8 / NT;                                 // bit slices
     constexpr int NW = NS * KG;
     constexpr bool SC = DPF_FOLD_SEL_CHEAP >= 0 ? DPF_FOLD_SEL_CHEAP == 1 : NT < MT;
@@ -792,6 +812,16 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[m][j][e] = 0.0f;
+    uint32_t since = 0;                                        // super-groups since the last parity reduction
+    auto to_parity = [&]() __attribute__((always_inline)) {
+        since = 0;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[m][j][e] -= 2.0f * __builtin_floorf(acc[m][j][e] * 0.5f);
+    };
     // One super-group: 4 K-blocks of 64 records x MT x NT MFMAs.
     auto fold_sg = [&](int sl, const uint4 (&B)[NT]) __attribute__((always_inline)) {
         uint4 A[MT];
@@ -835,6 +865,8 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
 #pragma unroll
         for (int sl = 0; sl < SG; ++sl)
             if ((uint64_t)sl < n) fold_sg(sl, Bc[sl]);
+        since += SG;
+        if (since >= par_every) to_parity();                   // uniform
     };
     uint64_t sb = s0;
     for (; sb + 2 * SG < s1; sb += 3 * SG) {
@@ -863,6 +895,8 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
 #pragma unroll
         for (int sl = 0; sl < SG; ++sl)
             if ((uint64_t)sl < n) fold_sg(sl, Bc[sl]);
+        since += SG;
+        if (since >= par_every) to_parity();                   // uniform
     };
     uint64_t sb = s0;
     for (; sb + SG < s1; sb += 2 * SG) {
@@ -1008,15 +1042,16 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
     }();
     uint64_t spb;
     split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
+    const uint32_t pe = fold_par_every();
     if (sgm_keys && sgm_g == 4)
         hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 4>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, sgm_keys);
+                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, pe, sgm_keys);
     else if (sgm_keys)
         hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 1>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, sgm_keys);
+                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, pe, sgm_keys);
     else
         hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words);
+                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, pe);
     return hipGetLastError();
 }
 }  // namespace
@@ -1088,6 +1123,10 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
     return hipSuccess;
 }
 
+#ifndef DPF_PIR_FUSED_KERNEL
+#define DPF_PIR_FUSED_KERNEL 0   // k_pir_fused is built only in the experimental build (make experimental)
+#endif
+#if DPF_PIR_FUSED_KERNEL
 // ---------------------------------------------------------------------------
 // Fused PIR answer: the subtree EvalFull and the matrix-core fold in ONE
 // launch, so the fold's MFMA and HBM streams could run under the tree's
@@ -1153,8 +1192,14 @@ struct FzCtx {
 };
 
 // Workgroup-scope flags in LDS (ASYNC ring).  Every wait is bounded, so each
-// wave reaches its exit even if a flag were never set.
+// wave reaches its exit even if a flag were never set; a wait that runs out
+// records it in g_fz_timeout (a vector atomic), and the next launch_pir_fused
+// reports hipErrorLaunchTimeOut instead of launching (the answers of the
+// timed-out launch are not to be trusted).  All 16 waves of the workgroup
+// are resident on one CU, so no wait should ever run out.
 constexpr uint32_t kFzSpin = 1u << 22;
+__device__ uint32_t g_fz_timeout;
+__device__ __forceinline__ void fz_timed_out() { atomicOr(&g_fz_timeout, 1u); }
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1190,7 +1235,7 @@ __device__ __forceinline__ void fz_emit(FzCtx& c, const Node& n) {
         // pair i - 2 (ring entry (i - 2) * kFzProd + p in folding order).
         if (i >= 2) {
             const uint32_t need = (i - 2) * kFzProd + c.p + 1;
-            for (uint32_t n = 0; n < kFzSpin; ++n) {
+            for (uint32_t n = 0;; ++n) {
                 uint32_t lo_ = lds_acquire(c.fold);
 #pragma unroll
                 for (int f = 1; f < kFzFold; ++f) {
@@ -1198,6 +1243,10 @@ __device__ __forceinline__ void fz_emit(FzCtx& c, const Node& n) {
                     lo_ = v < lo_ ? v : lo_;
                 }
                 if (lo_ >= need) break;
+                if (n == kFzSpin) {
+                    if ((threadIdx.x & 63) == 0) fz_timed_out();
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -1357,7 +1406,13 @@ __global__ __launch_bounds__(kFzThreads, 1) void k_pir_fused(const uint32_t* __r
         const bool has = fz_a0(p) + t < fz_a0(p + 1);           // producer p has a pair t (uniform)
         if constexpr (ASYNC) {
             if (has)
-                for (uint32_t n = 0; n < kFzSpin && lds_acquire(s_prod + p) <= t; ++n) __builtin_amdgcn_s_sleep(1);
+                for (uint32_t n = 0; lds_acquire(s_prod + p) <= t; ++n) {
+                    if (n == kFzSpin) {
+                        if (l == 0) fz_timed_out();
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
         }
         const uint32_t* rows = s_ring + (t & 1) * kFzSlot + p * 64 * kFzRow;
         uint4 A[2];   // stale when !has: the DB words are zero then (e2m1 has no NaN/Inf)
@@ -1417,6 +1472,13 @@ bool pir_fused_ok(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits, bool any_
 hipError_t launch_pir_fused(const uint32_t* ek, uint32_t nkeys, uint32_t stop, uint32_t prefix_bits, uint64_t prefix,
                             const uint8_t* dbs, uint64_t nrec, uint32_t* ans, uint32_t* parts, hipStream_t st) {
     if (!pir_fused_ok(nkeys, stop, prefix_bits, true)) return hipErrorInvalidValue;
+    uint32_t timed_out = 0;   // a ring wait of an earlier launch ran out (synchronises: test builds only)
+    if (hipMemcpyFromSymbol(&timed_out, HIP_SYMBOL(g_fz_timeout), sizeof timed_out) != hipSuccess) return hipErrorUnknown;
+    if (timed_out) {
+        const uint32_t z = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fz_timeout), &z, sizeof z);
+        return hipErrorLaunchTimeOut;
+    }
     if (nrec == 0) return hipMemsetAsync(ans, 0, (size_t)nkeys * 32, st);
     const uint64_t nsg = (nrec + 255) / 256;
     const uint32_t blocks = 1u << (stop - 1 - kFzBlockLog - prefix_bits);
@@ -1438,6 +1500,14 @@ hipError_t launch_pir_fused(const uint32_t* ek, uint32_t nkeys, uint32_t stop, u
                        64u, 8u, ans, (uint64_t)8, 0u);
     return hipGetLastError();
 }
+
+#else
+bool pir_fused_ok(uint64_t, uint32_t, uint32_t, bool) { return false; }
+hipError_t launch_pir_fused(const uint32_t*, uint32_t, uint32_t, uint32_t, uint64_t, const uint8_t*, uint64_t, uint32_t*,
+                            uint32_t*, hipStream_t) {
+    return hipErrorInvalidValue;
+}
+#endif  // DPF_PIR_FUSED_KERNEL
 
 FoldPlan plan_fold(uint64_t rec_bytes, uint32_t nkeys) {
     FoldPlan p{};

@@ -41,11 +41,19 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
                                   uint32_t nkeys, uint32_t* ans, uint32_t* parts, hipStream_t st,
                                   uint32_t sgm_keys = 0, uint32_t sgm_g = 1);
 
+// Tuning / test limits of the fold launches: at most max_blocks workgroups
+// per launch (0 = the default, 1024), and the matrix-core fold reduces its
+// fp32 counts to parities every par_every super-groups (0 = the default and
+// maximum, 2^15 = 2^23 records; counts stay below fp32's exact 2^24).
+void set_fold_limits(uint32_t max_blocks, uint32_t par_every);
+
 // Fused PIR answer (k_pir_fused): the subtree EvalFull of keys [0, nkeys)
 // from their expanded records (launch_unpack) and the matrix-core fold over
 // the sliced DB in one launch; where pir_fused_ok() (<= 64 keys, 2^8 .. 2^10
 // blocks of 256 leaf pairs in the subtree; any_size: from one block, for
-// tests).  Same ans / parts contract.
+// tests).  Same ans / parts contract.  Built only with DPF_PIR_FUSED_KERNEL=1
+// (make experimental): measured slower than the two launches;
+// otherwise pir_fused_ok() is false and the launcher refuses.
 bool pir_fused_ok(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits, bool any_size = false);
 hipError_t launch_pir_fused(const uint32_t* ek, uint32_t nkeys, uint32_t stop, uint32_t prefix_bits, uint64_t prefix,
                             const uint8_t* dbs, uint64_t nrec, uint32_t* ans, uint32_t* parts, hipStream_t st);

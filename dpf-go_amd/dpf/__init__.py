@@ -99,6 +99,7 @@ SIGNATURES = {
     "dpf_pir_db_slice_dev": (_int, [_int, _vp, _u64, _vp, _vp]),
     "dpf_pir_answer_sliced_dev": (_int, [_int, _vp, _sz, _sz, _u32, _u32, _u64, _vp, _u64, _vp, _vp, _vp]),
     "dpf_xor_fold_sliced_dev": (_int, [_int, _vp, _sz, _sz, _vp, _u64, _vp, _vp, _vp]),
+    "dpf_set_fold_limits": (_int, [_u32, _u32]),
     "dpf_pir_db_create": (_int, [_u8p, _u64, _u32, _int, ctypes.POINTER(_vp)]),
     "dpf_pir_answer": (_int, [_vp, _u8p, _sz, _sz, _u8p]),
     "dpf_pir_db_free": (None, [_vp]),
@@ -322,7 +323,7 @@ def evalfull_split(key: bytes, logN: int, ngpus: int, out: Optional[np.ndarray] 
 
 # --------------------------------------------- device-resident (torch) ---
 def _ptr(t) -> int:
-    return int(t.data_ptr())
+    return 0 if t is None else int(t.data_ptr())
 
 
 def _stream_handle(stream) -> int:
@@ -503,6 +504,13 @@ def xor_fold_sliced_dev(d_bits, bits_stride: int, nkeys: int, d_dbs, nrec: int, 
     """xor_fold_dev for 32-B records over the bit-sliced DB (the matrix-core fold)."""
     _check(lib().dpf_xor_fold_sliced_dev(device, _ptr(d_bits), bits_stride, nkeys, _ptr(d_dbs), nrec, _ptr(d_ans),
                                          _ptr(d_work), _stream_handle(stream)))
+
+
+def set_fold_limits(max_blocks: int = 0, parity_every: int = 0) -> None:
+    """Tuning / test limits of the fold launches (0 = default): workgroups per
+    launch, and super-groups between the matrix-core fold's parity reductions
+    (dpf_set_fold_limits).  Answers do not depend on them."""
+    _check(lib().dpf_set_fold_limits(max_blocks, parity_every))
 
 
 class PirDB:

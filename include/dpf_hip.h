@@ -166,8 +166,11 @@ int dpf_get_eval_kernel(void);
  * (dpf.go:171, :243).  DPF_SMALL_AUTO (default) evaluates them on the host's
  * AES units (host_eval.cpp: AES-NI/VAES, bit-exact with the kernels) when
  * that beats a GPU round trip: every dpf_eval, and dpf_evalfull up to
- * logN = dpf_small_call_max_logN(); DPF_SMALL_GPU always uses the GPU,
- * DPF_SMALL_HOST the host whenever it has AES-NI.  Either way a gfx950
+ * logN = dpf_small_call_max_logN(), which depends on the host (21 with
+ * VAES, 19 with AES-NI only); DPF_SMALL_GPU always uses the GPU,
+ * DPF_SMALL_HOST the host whenever it has AES-NI, except dpf_evalfull above
+ * logN = 28 (outputs of 32 MiB and more), which stays on the GPU.  Either
+ * way a gfx950
  * device must be open (DPF_ERR_NODEV otherwise): this is a latency path,
  * not a fallback.  The batched and _dev entry points always run on the GPU.
  * Process-wide; default from env DPF_SMALL_CALLS=auto|gpu|host. */
@@ -248,6 +251,14 @@ int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t key_len,
                               uint8_t* d_ans, void* d_work, void* stream);
 int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_stride, size_t nkeys, const uint8_t* d_dbs,
                             uint64_t nrec, uint8_t* d_ans, void* d_work, void* stream);
+/* Tuning / test limits of the XOR fold launches (process-wide; 0 = default):
+ * at most max_blocks workgroups per fold launch (default and maximum 1024),
+ * and the matrix-core fold reduces its fp32 counts to parities every
+ * parity_every super-groups of 256 records (default and maximum 2^15, so a
+ * count never exceeds 2^24, fp32's exact-integer bound, however many records
+ * a workgroup folds).  Answers do not depend on either; tests use them to
+ * force long per-workgroup runs and frequent reductions.  Returns 0. */
+int dpf_set_fold_limits(uint32_t max_blocks, uint32_t parity_every);
 /* Kernel shape of dpf_pir_answer_sliced_dev (and of a sliced PIR handle):
  * DPF_PIR_SPLIT (default): a tree launch writes the selection bits to HBM
  * and a fold launch reads them back.  DPF_PIR_FUSED: where nkeys <= 64 and

@@ -192,3 +192,91 @@ def test_sliced_pir_answer_two_server_full_size():
         rec = res[0] ^ res[1]
         for i in range(nk):
             assert np.array_equal(rec[i], db[int(al[i])]), (nk, i)
+
+
+@pytest.fixture
+def fold_limits():
+    yield dpf.set_fold_limits
+    dpf.set_fold_limits(0, 0)
+
+
+# the MFMA fold's answer bits are parities of fp32 counts, exact
+# only while a count stays <= 2^24.  The fold reduces its accumulators to
+# parities every `parity_every` super-groups, so a workgroup's run length no
+# longer matters.  Forced long runs (1-3 workgroups for the whole DB) and
+# reductions after every 1 / 3 / 5 super-groups must all give the answers of
+# the default shape and of the LDS fold over the row-major DB.
+@pytest.mark.parametrize("max_blocks,par_every,nk,nrec", [
+    (1, 1, 64, 8192), (3, 5, 33, 30000 - 7), (2, 3, 129, 20000), (1, 0, 256, 65536), (7, 2, 1, 9999),
+])
+def test_sliced_fold_forced_long_runs_and_parity_reductions(fold_limits, max_blocks, par_every, nk, nrec):
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(nk * 7 + nrec)
+    stride = ((nrec + 7) // 8 + 15) // 16 * 16
+    bits = rng.integers(0, 256, (nk, stride), dtype=np.uint8)
+    payload = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    d_bits = torch.from_numpy(bits.reshape(-1)).to(dev)
+    d_db = torch.from_numpy(payload.reshape(-1)).to(dev)
+    d_dbs = torch.empty(dpf.pir_db_sliced_size(nrec), dtype=torch.uint8, device=dev)
+    dpf.pir_db_slice_dev(d_db, nrec, d_dbs)
+    d_work = torch.empty(dpf.xor_fold_workspace_size(), dtype=torch.uint8, device=dev)
+
+    def run():
+        d_ans = torch.full((nk * 32,), 0xAB, dtype=torch.uint8, device=dev)
+        dpf.xor_fold_sliced_dev(d_bits, stride, nk, d_dbs, nrec, d_ans, d_work)
+        torch.cuda.synchronize()
+        return d_ans.cpu().numpy().reshape(nk, 32)
+
+    base = run()
+    fold_limits(max_blocks, par_every)
+    assert np.array_equal(run(), base)
+    fold_limits(0, 0)
+    assert np.array_equal(base, _fold(d_bits, stride, nk, payload, nrec, 32))
+    if nk <= 64:
+        assert np.array_equal(base, _want(bits, payload, nrec))
+
+
+def test_sliced_fold_counts_past_2p24_in_one_workgroup(fold_limits):
+    """One workgroup folds 2^24 + 2^21 records of an all-ones DB under
+    selection words that are mostly ones: every count passes 2^24 (fp32's
+    last exact integer, where a plain fp32 accumulation would round odd
+    partial sums), and the answer bit must be the parity of the number of
+    selected records."""
+    import torch
+    dev = torch.device("cuda", 0)
+    nk, nrec = 32, (1 << 24) + (1 << 21)
+    stride = nrec // 8
+    rng = np.random.default_rng(5)
+    bits = np.full((nk, stride), 0xFF, np.uint8)
+    holes = rng.random((nk, stride)) < 0.125
+    bits[holes] = rng.integers(0, 256, int(holes.sum()), dtype=np.uint8)
+    d_bits = torch.from_numpy(bits.reshape(-1)).to(dev)
+    d_dbs = torch.full((dpf.pir_db_sliced_size(nrec),), 0xFF, dtype=torch.uint8, device=dev)
+    d_work = torch.empty(dpf.xor_fold_workspace_size(), dtype=torch.uint8, device=dev)
+    d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=dev)
+    fold_limits(1, 0)
+    dpf.xor_fold_sliced_dev(d_bits, stride, nk, d_dbs, nrec, d_ans, d_work)
+    torch.cuda.synchronize()
+    got = d_ans.cpu().numpy().reshape(nk, 32)
+    par = np.unpackbits(bits, axis=1).sum(axis=1) & 1
+    want = np.where(par[:, None] == 1, 0xFF, 0).astype(np.uint8) * np.ones((1, 32), np.uint8)
+    assert np.array_equal(got, want)
+
+
+def test_pir_answer_rejects_bad_buffers():
+    """null or misaligned device buffers are DPF_ERR_PARAM at the
+    C ABI of both PIR answer entry points, not a GPU fault."""
+    import torch
+    logN, nk = 12, 2
+    _, ka, _ = _keys(nk, logN, first=5)
+    kl = dpf.key_len(logN)
+    d_keys = torch.from_numpy(ka.reshape(-1)).to("cuda")
+    d = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    w = torch.empty(dpf.pir_workspace_size(nk, logN), dtype=torch.uint8, device="cuda")
+    for f in (dpf.pir_answer_dev, dpf.pir_answer_sliced_dev):
+        for db, ans, work in ((None, d, w), (d, None, w), (d, d, None), (d[1:], d, w), (d, d[2:], w),
+                              (d, d, w[4:])):
+            with pytest.raises(dpf.DPFPanic) as e:
+                f(d_keys, kl, nk, logN, db, 100, ans, work)
+            assert e.value.code == dpf.DPF_ERR_PARAM

@@ -141,6 +141,122 @@ def test_config4_eight_db_slices_logN24():
         assert np.array_equal(rec[i], db[int(al[i])]), i
 
 
+@pytest.fixture(scope="module")
+def cfg4():
+    """configs[4]'s inputs (logN=24, 2^24 x 32 B synthetic DB, B=64 keys of
+    bench.py's seed) and the 1-GPU answers of the product path: the matrix-core
+    fold over the whole bit-sliced DB (prefix_bits=0)."""
+    import torch
+    logN, nk = 24, 64
+    nrec = 1 << logN
+    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    al, s0, s1 = synth.key_seeds(nk, logN, first=4242)
+    ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+    dev = torch.device("cuda", 0)
+    d_db = torch.from_numpy(db.reshape(-1)).to(dev)
+    d_dbs = torch.empty(dpf.pir_db_sliced_size(nrec), dtype=torch.uint8, device=dev)
+    dpf.pir_db_slice_dev(d_db, nrec, d_dbs, stream=_stream())
+    d_work = torch.empty(dpf.pir_workspace_size(nk, logN, 0), dtype=torch.uint8, device=dev)
+    d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=dev)
+    whole = []
+    for k in (ka, kb):
+        d_k = torch.from_numpy(k.reshape(-1)).to(dev)
+        dpf.pir_answer_sliced_dev(d_k, dpf.key_len(logN), nk, logN, d_dbs, nrec, d_ans, d_work, stream=_stream())
+        torch.cuda.synchronize()
+        whole.append(d_ans.cpu().numpy().reshape(nk, 32).copy())
+    dpf.forget_workspace(d_work)
+    del d_dbs, d_work
+    return {"logN": logN, "nk": nk, "nrec": nrec, "db": db, "al": al, "ka": ka, "kb": kb, "d_db": d_db,
+            "whole_a": whole[0], "whole_b": whole[1]}
+
+
+@pytest.mark.parametrize("pb", [1, 2, 3])
+def test_config4_sliced_product_path_per_rank(cfg4, pb):
+    """The N = 2^pb PIR rank's product path, as bench.py --gpus N --workload
+    pir runs it (pir_setup / pir_time): rank r bit-slices its DB slice
+    [r*2^(24-pb), (r+1)*2^(24-pb)) once (dpf_pir_db_slice_dev on d_db[lo:hi])
+    and answers with dpf_pir_answer_sliced_dev(prefix_bits=pb, prefix=r):
+    subtree r of every key (dpf/dpf.go:213-241 below the prefix) folded on the
+    matrix cores.  Keys 0 and 63 of every rank vs the oracle's XOR inner
+    product over that slice (dpf.go:243-262 bits), the partials XOR to the
+    1-GPU sliced answer, and the two servers XOR to DB[alpha]."""
+    import torch
+    logN, nk, nrec, db = cfg4["logN"], cfg4["nk"], cfg4["nrec"], cfg4["db"]
+    ka, kb, d_db = cfg4["ka"], cfg4["kb"], cfg4["d_db"]
+    kl = dpf.key_len(logN)
+    dev = torch.device("cuda", 0)
+    W = 1 << pb
+    d_keys = [torch.from_numpy(k.reshape(-1)).to(dev) for k in (ka, kb)]
+    d_work = torch.empty(dpf.pir_workspace_size(nk, logN, pb), dtype=torch.uint8, device=dev)
+    d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=dev)
+    acc = [np.zeros((nk, 32), np.uint8), np.zeros((nk, 32), np.uint8)]
+    for r in range(W):
+        pb_r, prefix = shard.subtree_split(W, r)
+        assert (pb_r, prefix) == (pb, r)
+        lo, hi = shard.db_slice(nrec, logN, W, r)
+        assert (lo, hi) == (r << (logN - pb), (r + 1) << (logN - pb))
+        d_dbs = torch.empty(dpf.pir_db_sliced_size(hi - lo), dtype=torch.uint8, device=dev)
+        dpf.pir_db_slice_dev(d_db[lo * 32:hi * 32], hi - lo, d_dbs, stream=_stream())
+        parts = []
+        for d_k in d_keys:
+            d_ans.fill_(0xA5)                                   # overwritten, not accumulated
+            dpf.pir_answer_sliced_dev(d_k, kl, nk, logN, d_dbs, hi - lo, d_ans, d_work, prefix_bits=pb,
+                                      prefix=prefix, stream=_stream())
+            torch.cuda.synchronize()
+            parts.append(d_ans.cpu().numpy().reshape(nk, 32).copy())
+        for i in (0, nk - 1):
+            want = np.frombuffer(oracle.pir_answer(ka[i].tobytes(), logN, db[lo:hi], lo, hi - lo), np.uint8)
+            assert np.array_equal(parts[0][i], want), (r, i)
+        acc[0] ^= parts[0]
+        acc[1] ^= parts[1]
+        del d_dbs
+    dpf.forget_workspace(d_work)
+    assert np.array_equal(acc[0], cfg4["whole_a"])
+    assert np.array_equal(acc[1], cfg4["whole_b"])
+    rec = acc[0] ^ acc[1]
+    for i in range(nk):
+        assert np.array_equal(rec[i], db[int(cfg4["al"][i])]), i
+
+
+def test_config4_pirdb_handle_on_eight_logical_devices():
+    """PirDB(db, 24, ngpus=8): the library's own 8-way sharded PIR handle at
+    the full configs[4] shape (8 bit-sliced 64 MiB shards, one per logical
+    device on this GPU, host XOR of the 8 partials), against the 1-GPU handle
+    and the 2-server property.  In a subprocess: the device registry is
+    process-wide."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import sys; sys.path[:0] = [%r, %r]
+import numpy as np, dpf, oracle
+from dpf import synth
+assert dpf.gpu_init_devices([0] * 8) == 8
+logN, nk = 24, 64
+nrec = 1 << logN
+db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+al, s0, s1 = synth.key_seeds(nk, logN, first=8080)
+ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+p8 = dpf.PirDB(db, logN, ngpus=8)
+a8, b8 = p8.answer(ka), p8.answer(kb)
+p8.close()
+p1 = dpf.PirDB(db, logN, ngpus=1)
+a1 = p1.answer(ka)
+p1.close()
+assert np.array_equal(a8, a1)
+rec = a8 ^ b8
+for i in range(nk):
+    assert np.array_equal(rec[i], db[int(al[i])]), i
+for i in (0, nk - 1):
+    assert a8[i].tobytes() == oracle.pir_answer(ka[i].tobytes(), logN, db, 0, nrec), i
+dpf.gpu_shutdown()
+print("done")
+''' % (os.path.join(root, "dpf-go_amd"), os.path.join(root, "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.strip().endswith("done")
+
+
 def test_library_multi_device_entry_points_with_every_opened_device():
     """dpf_evalfull_split and the PIR handle with ngpus = the opened devices
     (1 on a 1-GPU box; the same code shards over 8 on a full node)."""

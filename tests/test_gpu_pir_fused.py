@@ -1,8 +1,12 @@
-"""GPU parity of the fused PIR kernel (k_pir_fused: subtree EvalFull and the
-matrix-core fold in one launch) against the CPU oracle's XOR
-inner product over EvalFull bits (dpf/dpf.go:213-262 for the bits), against
-the two-launch path on the same inputs, and the 2-server property at the
-configs[4] shape (logN=24, 2^24 x 32 B DB)."""
+"""GPU parity of the sliced PIR answer over subtree slices (the two-launch
+product path: tree kernel, then the matrix-core fold) and of the fused PIR
+kernel (k_pir_fused: subtree EvalFull and the matrix-core fold in one launch,
+DESIGN.md §4.4) against the CPU oracle's XOR inner product over EvalFull bits
+(dpf/dpf.go:213-262 for the bits), and the 2-server property at the configs[4]
+shape (logN=24, 2^24 x 32 B DB).  The fused kernel is in the experimental
+build only (make -C dpf-go_amd experimental; run these tests with
+DPF_LIB=dpf-go_amd/lib/variants/libdpf_hip_exp.so): with the product library
+its legs are skipped."""
 import numpy as np
 import pytest
 
@@ -18,11 +22,23 @@ def _gpu():
     assert dpf.gpu_init(1) >= 1
 
 
+def _fused_built() -> bool:
+    try:
+        prev = dpf.set_pir_kernel("fused-any")
+    except dpf.DPFPanic:
+        return False
+    dpf.set_pir_kernel(prev)
+    return True
+
+
 @pytest.fixture
 def pir_kernel():
     prev = dpf.get_pir_kernel()
     yield dpf.set_pir_kernel
     dpf.set_pir_kernel(prev)
+
+
+needs_fused = pytest.mark.skipif("not _fused_built()", reason="k_pir_fused is in the experimental build only")
 
 
 def _keys(nk, logN, first=0):
@@ -64,6 +80,18 @@ SHAPES = [
 
 
 @pytest.mark.parametrize("logN,nrec,nk,pb,prefix", SHAPES)
+def test_sliced_split_matches_oracle(pir_kernel, logN, nrec, nk, pb, prefix):
+    slice_n = 1 << (logN - pb)
+    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    _, ka, _ = _keys(nk, logN, first=logN + nk)
+    want = np.stack([np.frombuffer(oracle.pir_answer(ka[i].tobytes(), logN, db, prefix * slice_n, nrec), np.uint8)
+                     for i in range(nk)])
+    pir_kernel("split")
+    assert np.array_equal(_answer(ka, logN, db, nrec, pb, prefix), want)
+
+
+@needs_fused
+@pytest.mark.parametrize("logN,nrec,nk,pb,prefix", SHAPES)
 def test_fused_matches_oracle(pir_kernel, logN, nrec, nk, pb, prefix):
     slice_n = 1 << (logN - pb)
     db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
@@ -73,10 +101,9 @@ def test_fused_matches_oracle(pir_kernel, logN, nrec, nk, pb, prefix):
     want = np.stack([np.frombuffer(oracle.pir_answer(ka[i].tobytes(), logN, db, prefix * slice_n, nrec), np.uint8)
                      for i in range(nk)])
     assert np.array_equal(got, want)
-    pir_kernel("split")
-    assert np.array_equal(_answer(ka, logN, db, nrec, pb, prefix), want)
 
 
+@needs_fused
 def test_fused_at_configs4_recovers_records(pir_kernel):
     """configs[4] on one GPU (logN=24, 2^24 x 32 B, 64 keys) through the
     fused kernel: answer(ka) ^ answer(kb) == DB[alpha] and the answers equal
@@ -111,3 +138,10 @@ def test_pir_kernel_switch(pir_kernel):
     assert pir_kernel(prev) == dpf.PIR_SPLIT
     with pytest.raises(Exception):
         pir_kernel(7)
+    if not _fused_built():
+        # product build: the fused kernel is refused, and every shape runs split
+        with pytest.raises(dpf.DPFPanic) as e:
+            pir_kernel("fused")
+        assert e.value.code == dpf.DPF_ERR_PARAM
+        assert dpf.get_pir_kernel() == dpf.PIR_SPLIT
+        assert dpf.pir_kernel_for(64, 24) == dpf.PIR_SPLIT
