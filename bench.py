@@ -460,7 +460,101 @@ def wl_evalfull(c: Ctx) -> dict:
     if c.world == 1 and not a.no_api:
         line["api"] = api_rates(c, ka, logN)
         line["single_call"] = single_call_latency(c, ka[0].tobytes(), logN)
+        c.reference_shapes = reference_shapes_gpu(c)
     return line
+
+
+# The reference's own timing shapes: BenchmarkEvalFull is one
+# EvalFull at logN=28 of a key for alpha=0 (dpf/dpf_test.go:7-21); the CLI
+# times Gen(123, 27) then 100 x EvalFull(., 27) (dpf_main.go:25-30).  The GPU
+# side runs them through the drop-in single-key API (dpf.EvalFull, a fresh
+# output like the Go slice, dpf.go:251) and kernel-resident (one key's
+# dpf_evalfull_batch_dev, output left in HBM); the CPU side (finalize) is the
+# oracle's reference-style restatement on one core.
+REF_SHAPES = {"BenchmarkEvalFull": {"logN": 28, "alpha": 0, "source": "dpf/dpf_test.go:7-21"},
+              "dpf_main": {"logN": 27, "alpha": 123, "reps": 100, "source": "dpf_main.go:25-30"}}
+
+
+def reference_shapes_gpu(c: Ctx) -> dict:
+    dpf, torch = c.dpf, c.torch
+    out = {}
+    for name, sh in REF_SHAPES.items():
+        logN = sh["logN"]
+        al, s0, s1 = np.array([sh["alpha"]], np.uint64), *[np.frombuffer(bytes(range(i, i + 16)), np.uint8)[None]
+                                                           for i in (1, 17)]
+        ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+        key = ka[0].tobytes()
+        d_key = torch.from_numpy(ka.reshape(-1)).to(c.dev)
+        d_work = torch.empty(dpf.workspace_size(1, logN), dtype=torch.uint8, device=c.dev)
+        d_out = torch.empty(dpf.evalfull_len(logN), dtype=torch.uint8, device=c.dev)
+
+        def dev_call():
+            dpf.evalfull_batch_dev(d_key, len(key), 1, logN, d_out, d_work, device=c.local, stream=c.stream)
+        for _ in range(3):
+            dev_call()
+        torch.cuda.synchronize(c.dev)
+        reps = sh.get("reps", 20)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dev_call()
+        torch.cuda.synchronize(c.dev)
+        dev_ms = (time.perf_counter() - t0) / reps * 1e3
+        dpf.EvalFull(key, logN)                                  # warm the host-buffer path
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dpf.EvalFull(key, logN)
+        api_ms = (time.perf_counter() - t0) / reps * 1e3
+        r = {"logN": logN, "alpha": sh["alpha"], "source": sh["source"],
+             "gpu_dev_ms_per_evalfull": round(dev_ms, 4),
+             "gpu_api_ms_per_evalfull": round(api_ms, 4),
+             "gpu_dev_points_per_s": (1 << logN) / (dev_ms * 1e-3),
+             "gpu_note": "dev: dpf_evalfull_batch_dev of one key, output left in HBM; api: dpf.EvalFull "
+                         "(C ABI dpf_evalfull, fresh host output incl. its D2H), mean of %d calls" % reps}
+        if name == "dpf_main":
+            t0 = time.perf_counter()
+            k2, _ = dpf.Gen(123, logN)
+            for _ in range(reps):
+                dpf.EvalFull(k2, logN)
+            r["gpu_api_total_s"] = round(time.perf_counter() - t0, 4)
+            r["gpu_api_total_note"] = "Gen(123, 27) + 100 x EvalFull(., 27) through the drop-in API, as dpf_main.go"
+        out[name] = r
+    return out
+
+
+def reference_shapes_cpu(gpu: dict) -> dict:
+    """The same shapes on ONE host core with the oracle's reference-style
+    restatement (AES-NI, one aes128MMO per call, DFS: dpf.go:213-262), beside
+    the GPU numbers of reference_shapes_gpu."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    out = {}
+    for name, sh in REF_SHAPES.items():
+        logN = sh["logN"]
+        ka, _ = oracle.gen(sh["alpha"], logN, bytes(range(1, 17)), bytes(range(17, 33)))
+        r = dict(gpu.get(name, {"logN": logN, "alpha": sh["alpha"], "source": sh["source"]}))
+        if name == "dpf_main":
+            t0 = time.perf_counter()
+            k, _ = oracle.gen(123, logN, bytes(range(1, 17)), bytes(range(17, 33)))
+            for _ in range(sh["reps"]):
+                oracle.evalfull(k, logN, aesni=True)
+            tot = time.perf_counter() - t0
+            r["cpu_total_s"] = round(tot, 3)
+            r["cpu_ms_per_evalfull"] = round(tot / sh["reps"] * 1e3, 3)
+        else:
+            oracle.evalfull(ka, logN, aesni=True)
+            reps, t0 = 0, time.perf_counter()
+            while reps < 3 or time.perf_counter() - t0 < 2.0:
+                oracle.evalfull(ka, logN, aesni=True)
+                reps += 1
+            r["cpu_ms_per_evalfull"] = round((time.perf_counter() - t0) / reps * 1e3, 3)
+            r["cpu_reps"] = reps
+        r["cpu_cores"] = 1
+        r["cpu_kind"] = "port (oracle/dpf_oracle.c, AES-NI one block per call, DFS)"
+        if "gpu_dev_ms_per_evalfull" in r:
+            r["gpu_dev_speedup_vs_cpu"] = round(r["cpu_ms_per_evalfull"] / r["gpu_dev_ms_per_evalfull"], 1)
+            r["gpu_api_speedup_vs_cpu"] = round(r["cpu_ms_per_evalfull"] / r["gpu_api_ms_per_evalfull"], 1)
+        out[name] = r
+    return out
 
 
 def single_call_latency(c: Ctx, key: bytes, logN: int) -> dict:
@@ -1002,6 +1096,7 @@ def main() -> None:
     if args.workload == "evalfull" and not (args.no_workloads or args.strong or args.emulate_world > 1):
         line["workloads"] = sub_workloads(c)
     if c.rank == 0:
+        args.ref_gpu = getattr(c, "reference_shapes", {})
         finalize(line, args, c.world, c.folded)
         print(json.dumps(line), flush=True)
     if c.world > 1:
@@ -1016,6 +1111,8 @@ def finalize(line: dict, args, world: int, folded: bool) -> None:
     if not args.no_cpu_baseline:
         if args.workload == "evalfull":
             line["cpu_baseline"] = cpu_baseline(args.logN, args.cpu_seconds)
+            if world == 1 and not args.no_api:
+                line["cpu_baseline"]["reference_shapes"] = reference_shapes_cpu(getattr(args, "ref_gpu", {}))
         elif args.workload == "split":
             line["cpu_baseline"] = cpu_baseline(20, min(args.cpu_seconds, 8.0))
             line["cpu_baseline"]["note"] = ("points/s of the batched EvalFull port at logN=20: the per-point "

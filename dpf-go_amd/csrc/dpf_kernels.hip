@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <mutex>
 #include "aes_consts.hpp"
 #include "aes_ttable.hpp"
 #include "dpf_kernels.hpp"
@@ -558,81 +559,105 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
 }
 
 // Batched Eval as a visited-node trie below the frontier.
-// A key's queries share prefixes: at configs[2] (1024 points per key,
-// stop 13) levels 10-13 hold only 647 / 806 / 906 / 963 distinct nodes and
-// 963 distinct leaf blocks, where per-query walks compute 1024 of each.
-// One 1024-thread workgroup (the CU's LDS: one 64 KiB table plus the trie
-// state) takes kTrieKeys keys:
-//   1. every query marks its node at each level L..stop in per-level bitmaps
-//      (LDS atomics), and one wave per (key, level) turns a bitmap into
-//      per-word prefix counts: rank(pos) = prefix[pos/32] + popc(bits below);
-//   2. the key's visited level-L nodes come from the HBM frontier (the NODES
-//      pass), stored by rank;
-//   3. per level l = L+1..stop, every visited child finds its parent's rank
-//      (map pass: thread per bitmap word, one entry per set bit), then all
-//      children are computed with one AES each (dpf.go:183-201's on-path
-//      child), reading every parent before any child overwrites the store;
-//      at l = stop the leaf MMO follows at once (dpf.go:214-224);
-//   4. each query reads bit x & 127 of its leaf block by rank.
-// AES per key at configs[2]: 1022 (frontier) + 4285 = 5307, against 6142
-// for frontier + per-query walks.  Output: one 0/1 byte per query, as k_eval.
-constexpr uint32_t kTrieKeys = 4;           // keys per workgroup
-constexpr uint32_t kTrieCap = 1024;         // nodes per key per level (pts_per_key <= kTrieCap)
-constexpr uint32_t kTrieBlock = 1024;       // threads per workgroup (16 waves: 4 per SIMD)
+// A key's queries share prefixes: at configs[2] (1024 points per key, stop
+// 13) levels 10-13 hold only 647 / 806 / 906 / 963 distinct nodes and 963
+// distinct leaf blocks, where per-query walks compute 1024 of each.
+//
+// r05 layout (k_eval_trie): one key per 512-thread workgroup, the shape and
+// LDS budget of k_eval2 (the 64 KiB table plus ~6 KiB of trie metadata: two
+// workgroups per CU).  The r04 kernel kept the node seeds of 4 keys in LDS
+// too (~88 KiB), so one workgroup filled a CU and every per-level barrier
+// idled it (24% slower than the walks).  Here the seeds of the level being
+// built live in a scratch slot in global memory that stays in the CU's L2:
+// the slot is named by the workgroup's hardware id (XCC, SE, SH, CU, TG
+// slot), which no two resident workgroups share, so every CU reuses the same
+// few slots and the nodes never need to reach HBM.
+//   1. each query marks its node at every level L+1..stop in per-level
+//      bitmaps (LDS atomics); one wave per level turns a bitmap into per-word
+//      prefix counts: rank(pos) = prefix[pos/32] + popc(bits below);
+//   2. per level l = L+1..stop: a map pass (thread per bitmap word) gives
+//      each visited node (by rank) its parent: a level-L frontier index
+//      (the NODES pass, in HBM) or the parent's rank; then every thread reads
+//      the parents of its (<= 2) nodes, a barrier, and computes them, one AES
+//      each: dpf.go:183-201's on-path child; at l = stop the leaf MMO and the
+//      final CW follow at once (dpf.go:214-224);
+//   3. each query reads bit x & 127 of its leaf block by rank.
+// AES per key at configs[2]: 1022 (frontier) + 4285 = 5307, against 6142 for
+// frontier + per-query walks; wave-AES per key 71 against 80 for k_eval2
+// (a wave runs its second AES of a level only if one of its lanes has two
+// nodes).  Output: one 0/1 byte per query, as k_eval.
+constexpr uint32_t kTrieBlock = 512;        // threads per workgroup (one key)
+constexpr uint32_t kTrieCap = 1024;         // points per key (and nodes per level)
+constexpr uint32_t kTrieItems = kTrieCap / kTrieBlock;   // nodes per thread per level (2)
 constexpr uint32_t kTrieMaxStop = 13;       // bitmaps: 2^l bits per level l <= 13
-constexpr uint32_t kTrieWords = 520;        // bitmap words per key, levels L..stop (<= 2^(stop-4) + levels)
-constexpr uint32_t kTrieItems = kTrieKeys * kTrieCap / kTrieBlock;   // children per thread per level (4)
+constexpr uint32_t kTrieWords = 512;        // bitmap words, levels L+1..stop (<= 2^(stop-4))
+constexpr uint32_t kTrieMaxLevels = 12;
+constexpr uint64_t kTrieSlots = 1ull << 15; // hardware workgroup ids: XCC 3 | SE 3 | SH 1 | CU 4 | TG 4 bits
 
-__device__ __forceinline__ uint32_t trie_words(uint32_t l) { return l >= 5 ? 1u << (l - 5) : 1u; }
+__host__ __device__ __forceinline__ uint32_t trie_words(uint32_t l) { return l >= 5 ? 1u << (l - 5) : 1u; }
 
-__global__ __launch_bounds__(kTrieBlock, 1) void k_eval_trie(const uint32_t* __restrict__ ekeys, uint32_t stop,
+// This workgroup's scratch slot: HW_ID (hwreg 4) fields CU_ID [11:8], SH_ID
+// [12], SE_ID [15:13], TG_ID [19:16], and XCC_ID (hwreg 20) [2:0].
+__device__ __forceinline__ uint32_t trie_slot() {
+    const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(0xF814) & 7u;
+    return (xcc << 12) | (((hw >> 13) & 7u) << 9) | (((hw >> 12) & 1u) << 8) | (((hw >> 8) & 15u) << 4) |
+           ((hw >> 16) & 15u);
+}
+
+__global__ __launch_bounds__(kTrieBlock, 4) void k_eval_trie(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                               uint32_t logN, const uint64_t* __restrict__ xs,
-                                                              uint64_t nkeys, uint32_t ppk,
-                                                              const uint4* __restrict__ fseed,
+                                                              uint32_t ppk, const uint4* __restrict__ fseed,
                                                               const uint8_t* __restrict__ ft, uint32_t L,
+                                                              uint4* __restrict__ scratch,
                                                               uint8_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-    __shared__ __attribute__((aligned(16))) uint4 s_node[kTrieKeys * kTrieCap];   // seeds (leaf blocks at the end)
-    __shared__ uint8_t s_t[kTrieKeys * kTrieCap];
-    __shared__ uint16_t s_map[kTrieKeys * kTrieCap];                              // parent rank * 2 + side
-    __shared__ uint32_t s_bm[kTrieKeys * kTrieWords];
-    __shared__ uint16_t s_pre[kTrieKeys * kTrieWords];
-    __shared__ uint32_t s_cnt[kTrieKeys][kTrieMaxStop + 2];                       // visited nodes per level
+    __shared__ uint32_t s_bm[kTrieWords];
+    __shared__ uint16_t s_pre[kTrieWords];
+    __shared__ uint16_t s_map[kTrieCap];          // parent (rank or frontier index) * 2 + side
+    __shared__ uint8_t s_t[kTrieCap];             // t bytes of the stored nodes, by rank
+    __shared__ uint32_t s_cnt[kTrieMaxLevels];    // visited nodes per level
     const uint32_t tid = threadIdx.x;
-    const uint64_t k0 = (uint64_t)blockIdx.x * kTrieKeys;
-    const uint32_t nk = (uint32_t)(nkeys - k0 < kTrieKeys ? nkeys - k0 : kTrieKeys);
-    const uint32_t npts = nk * ppk;
-    const uint64_t q0 = k0 * ppk;
-    // Word offset of level l's bitmap inside a key's kTrieWords.
+    const uint64_t key = blockIdx.x;
+    const uint64_t q0 = key * ppk;
+    uint4* const scr = scratch + (uint64_t)trie_slot() * kTrieCap;
+    const uint32_t* ek = ekeys + key * ((uint64_t)(stop + 2) * 8);
+    // Word offset of level l's bitmap (levels L+1..stop).
     auto woff = [&](uint32_t l) {
         uint32_t o = 0;
-        for (uint32_t i = L; i < l; ++i) o += trie_words(i);
+        for (uint32_t i = L + 1; i < l; ++i) o += trie_words(i);
         return o;
     };
     auto pos_at = [&](uint64_t x, uint32_t l) { return (uint32_t)(x >> (logN - l)) & ((1u << l) - 1u); };
-    auto rank = [&](uint32_t k, uint32_t wo, uint32_t p) {
-        const uint32_t w = k * kTrieWords + wo + (p >> 5);
+    auto rank = [&](uint32_t wo, uint32_t p) {
+        const uint32_t w = wo + (p >> 5);
         return (uint32_t)s_pre[w] + (uint32_t)__builtin_popcount(s_bm[w] & ((1u << (p & 31)) - 1u));
     };
-    for (uint32_t i = tid; i < kTrieKeys * kTrieWords; i += kTrieBlock) s_bm[i] = 0;
-    fill_table(s_tab);                                   // ends with a barrier
-    // 1. Mark every query's node at each level L..stop.
-    for (uint32_t i = tid; i < npts; i += kTrieBlock) {
-        const uint64_t x = xs[q0 + i];
-        const uint32_t k = i / ppk;
+    uint64_t x[kTrieItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kTrieItems; ++j) {
+        const uint32_t i = tid + j * kTrieBlock;
+        x[j] = i < ppk ? xs[q0 + i] : 0;                  // issued before the table fill
+    }
+    for (uint32_t i = tid; i < kTrieWords; i += kTrieBlock) s_bm[i] = 0;
+    fill_table(s_tab);                                    // ends with a barrier
+    // 1. Mark every query's node at each level L+1..stop.
+#pragma unroll
+    for (uint32_t j = 0; j < kTrieItems; ++j) {
+        if (tid + j * kTrieBlock >= ppk) continue;
         uint32_t wo = 0;
-        for (uint32_t l = L; l <= stop; ++l) {
-            const uint32_t p = pos_at(x, l);
-            atomicOr(&s_bm[k * kTrieWords + wo + (p >> 5)], 1u << (p & 31));
+        for (uint32_t l = L + 1; l <= stop; ++l) {
+            const uint32_t p = pos_at(x[j], l);
+            atomicOr(&s_bm[wo + (p >> 5)], 1u << (p & 31));
             wo += trie_words(l);
         }
     }
     __syncthreads();
-    {   // Prefix counts: one wave per (key, level) segment.
-        const uint32_t wave = tid >> 6, lane = tid & 63, nlev = stop - L + 1;
-        for (uint32_t sg = wave; sg < nk * nlev; sg += kTrieBlock / 64) {
-            const uint32_t k = sg / nlev, l = L + sg % nlev;
-            const uint32_t base = k * kTrieWords + woff(l), nw = trie_words(l);
+    {   // Prefix counts: one wave per level.
+        const uint32_t wave = tid >> 6, lane = tid & 63, nlev = stop - L;
+        for (uint32_t sg = wave; sg < nlev; sg += kTrieBlock / 64) {
+            const uint32_t l = L + 1 + sg;
+            const uint32_t base = woff(l), nw = trie_words(l);
             uint32_t carry = 0;
             for (uint32_t c = 0; c < nw; c += 64) {
                 const uint32_t w = c + lane;
@@ -646,108 +671,88 @@ __global__ __launch_bounds__(kTrieBlock, 1) void k_eval_trie(const uint32_t* __r
                 if (w < nw) s_pre[base + w] = (uint16_t)(carry + inc - v);
                 carry += __shfl(inc, 63, 64);
             }
-            if (lane == 0) s_cnt[k][l - L] = carry;
+            if (lane == 0) s_cnt[sg] = carry;
         }
     }
     __syncthreads();
-    // 2. The visited level-L nodes, by rank, from the HBM frontier.
-    for (uint32_t i = tid; i < (nk << L); i += kTrieBlock) {
-        const uint32_t k = i >> L, p = i & ((1u << L) - 1u);
-        const uint32_t w = k * kTrieWords + (p >> 5);
-        if ((s_bm[w] >> (p & 31)) & 1u) {
-            const uint32_t r = rank(k, 0, p);
-            const uint64_t idx = ((k0 + k) << L) + p;
-            s_node[k * kTrieCap + r] = fseed[idx];
-            s_t[k * kTrieCap + r] = ft[idx];
-        }
-    }
     const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
     const uint32_t lo = (tid & 31u) * 4u;
-    const uint64_t rec = (uint64_t)(stop + 2) * 8;
+    const Blk fcw = load_blk(ek + 8 + 8 * stop);
     uint32_t wo_par = 0;
     for (uint32_t l = L + 1; l <= stop; ++l) {
-        const uint32_t wo = wo_par + trie_words(l - 1), nw = trie_words(l);
-        // 3a. Map pass: child rank -> parent rank * 2 + side.
-        for (uint32_t i = tid; i < nk * nw; i += kTrieBlock) {
-            const uint32_t k = i / nw, w = i % nw;
-            uint32_t bits = s_bm[k * kTrieWords + wo + w];
-            uint32_t r = s_pre[k * kTrieWords + wo + w];
+        const uint32_t wo = l == L + 1 ? 0u : wo_par + trie_words(l - 1), nw = trie_words(l);
+        // 2a. Map pass: node rank -> parent * 2 + side.
+        for (uint32_t w = tid; w < nw; w += kTrieBlock) {
+            uint32_t bits = s_bm[wo + w];
+            uint32_t r = s_pre[wo + w];
             while (bits) {
                 const uint32_t b = (uint32_t)__builtin_ctz(bits);
                 bits &= bits - 1u;
                 const uint32_t c = 32u * w + b;
-                s_map[k * kTrieCap + r++] = (uint16_t)((rank(k, wo_par, c >> 1) << 1) | (c & 1u));
+                const uint32_t par = l == L + 1 ? c >> 1 : rank(wo_par, c >> 1);
+                s_map[r++] = (uint16_t)((par << 1) | (c & 1u));
             }
         }
         __syncthreads();
-        // 3b. Children: read every parent, then compute and store.
-        uint32_t off[kTrieKeys + 1];
-        off[0] = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kTrieKeys; ++k) off[k + 1] = off[k] + (k < nk ? s_cnt[k][l - L] : 0u);
+        // 2b. Parents of this thread's nodes (rank tid, tid + 512), then a
+        // barrier before any node of this level overwrites the slot.
+        const uint32_t cnt = s_cnt[l - L - 1];
         Node n[kTrieItems];
-        uint32_t kk[kTrieItems], jj[kTrieItems], side[kTrieItems];
+        uint32_t side[kTrieItems];
 #pragma unroll
-        for (uint32_t m = 0; m < kTrieItems; ++m) {
-            const uint32_t i = tid + m * kTrieBlock;
-            uint32_t k = 0;
-#pragma unroll
-            for (uint32_t z = 1; z < kTrieKeys; ++z) k += i >= off[z] ? 1u : 0u;
-            kk[m] = k;
-            jj[m] = i - off[k];
-            side[m] = 0;
-            n[m] = {{0, 0, 0, 0}, 0};
-            if (i < off[kTrieKeys]) {
-                const uint32_t v = s_map[k * kTrieCap + jj[m]];
-                const uint4 sd = s_node[k * kTrieCap + (v >> 1)];
-                n[m] = {{sd.x, sd.y, sd.z, sd.w}, s_t[k * kTrieCap + (v >> 1)]};
-                side[m] = v & 1u;
+        for (uint32_t j = 0; j < kTrieItems; ++j) {
+            const uint32_t r = tid + j * kTrieBlock;
+            n[j] = {{0, 0, 0, 0}, 0};
+            side[j] = 0;
+            if (r < cnt) {
+                const uint32_t v = s_map[r], par = v >> 1;
+                side[j] = v & 1u;
+                if (l == L + 1) {
+                    const uint64_t idx = (key << L) + par;
+                    const uint4 sd = fseed[idx];
+                    n[j] = {{sd.x, sd.y, sd.z, sd.w}, ft[idx]};
+                } else {
+                    const uint4 sd = scr[par];
+                    n[j] = {{sd.x, sd.y, sd.z, sd.w}, s_t[par]};
+                }
             }
         }
         __syncthreads();
-#pragma unroll
-        for (uint32_t m = 0; m < kTrieItems; m += 2) {
-            const uint32_t ia = tid + m * kTrieBlock, ib = ia + kTrieBlock;
-            if (ia >= off[kTrieKeys]) break;                       // ib >= ia: both past the end
-            const uint32_t* eka = ekeys + (k0 + kk[m]) * rec;
-            const uint32_t* ekb = ekeys + (k0 + kk[m + 1]) * rec;
-            const bool hb = ib < off[kTrieKeys];
-            // Valid items are the first off[kTrieKeys] of the level, so only
-            // one wave per slot pair is ragged: waves without a second item
-            // run one AES instead of two (the saving is per wave instruction).
-            if (__builtin_amdgcn_read_exec() & __ballot(hb)) {
-                walk_step2<DPF_EVAL_BATCH>(tab, lo, n[m], load_cw(eka, l - 1), side[m], n[m + 1],
-                                           load_cw(hb ? ekb : eka, l - 1), side[m + 1]);
-                if (l == stop) {                                   // leaf blocks (dpf.go:214-224)
-                    Blk oa, ob;
-                    mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n[m].s, oa, KeyFixed<false>{}, n[m + 1].s, ob);
-                    n[m].s = leaf_fix(oa, n[m].t, load_blk(eka + 8 + 8 * stop));
-                    n[m + 1].s = leaf_fix(ob, n[m + 1].t, load_blk((hb ? ekb : eka) + 8 + 8 * stop));
-                }
-            } else {
-                walk_step<DPF_EVAL_BATCH>(tab, lo, n[m], load_cw(eka, l - 1), side[m]);
-                if (l == stop)
-                    n[m].s = leaf_fix(mmo1<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n[m].s), n[m].t,
-                                      load_blk(eka + 8 + 8 * stop));
+        const CW cw = load_cw(ek, l - 1);
+        const uint32_t r1 = tid + kTrieBlock;
+        const bool has0 = tid < cnt, has1 = r1 < cnt;
+        // A wave runs the second AES of the level only if a lane has a
+        // second node (ranks are dense: only the first waves do).
+        if (__builtin_amdgcn_read_exec() & __ballot(has1)) {
+            walk_step2<DPF_EVAL_BATCH>(tab, lo, n[0], cw, side[0], n[1], cw, side[1]);
+            if (l == stop) {                                   // leaf blocks (dpf.go:214-224)
+                Blk oa, ob;
+                mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n[0].s, oa, KeyFixed<false>{}, n[1].s, ob);
+                n[0].s = leaf_fix(oa, n[0].t, fcw);
+                n[1].s = leaf_fix(ob, n[1].t, fcw);
             }
-            s_node[kk[m] * kTrieCap + jj[m]] = make_uint4(n[m].s.c0, n[m].s.c1, n[m].s.c2, n[m].s.c3);
-            s_t[kk[m] * kTrieCap + jj[m]] = (uint8_t)n[m].t;
-            if (hb) {
-                s_node[kk[m + 1] * kTrieCap + jj[m + 1]] =
-                    make_uint4(n[m + 1].s.c0, n[m + 1].s.c1, n[m + 1].s.c2, n[m + 1].s.c3);
-                s_t[kk[m + 1] * kTrieCap + jj[m + 1]] = (uint8_t)n[m + 1].t;
-            }
+        } else if (__builtin_amdgcn_read_exec() & __ballot(has0)) {
+            walk_step<DPF_EVAL_BATCH>(tab, lo, n[0], cw, side[0]);
+            if (l == stop) n[0].s = leaf_fix(mmo1<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, n[0].s), n[0].t, fcw);
+        }
+        if (has0) {
+            scr[tid] = make_uint4(n[0].s.c0, n[0].s.c1, n[0].s.c2, n[0].s.c3);
+            s_t[tid] = (uint8_t)n[0].t;
+        }
+        if (has1) {
+            scr[r1] = make_uint4(n[1].s.c0, n[1].s.c1, n[1].s.c2, n[1].s.c3);
+            s_t[r1] = (uint8_t)n[1].t;
         }
         wo_par = wo;
-        __syncthreads();   // children stored before the next map pass's parents are read (3b)
+        __syncthreads();   // this level's nodes stored before the next level reads them
     }
-    // 4. Each query's bit of its leaf block.
-    for (uint32_t i = tid; i < npts; i += kTrieBlock) {
-        const uint64_t x = xs[q0 + i];
-        const uint32_t k = i / ppk;
-        const uint32_t r = rank(k, wo_par, pos_at(x, stop));
-        const uint4 o = s_node[k * kTrieCap + r];
-        out[q0 + i] = eval_bit({o.x, o.y, o.z, o.w}, x);
+    // 3. Each query's bit of its leaf block.
+#pragma unroll
+    for (uint32_t j = 0; j < kTrieItems; ++j) {
+        const uint32_t i = tid + j * kTrieBlock;
+        if (i >= ppk) continue;
+        const uint4 o = scr[rank(wo_par, pos_at(x[j], stop))];
+        out[q0 + i] = eval_bit({o.x, o.y, o.z, o.w}, x[j]);
     }
 }
 
@@ -982,16 +987,19 @@ uint64_t eval_frontier_bytes(uint64_t nkeys, uint32_t stop, uint64_t pts_per_key
     return ((nkeys << L) * 16 + (nkeys << L) + 255) & ~255ull;
 }
 
-// The trie kernel's limits: every level's bitmap and nodes in LDS.
+// The trie kernel's limits: one key per workgroup, <= 1024 points (2 per
+// thread), every level's bitmap in LDS.
 static bool trie_ok(uint32_t stop, uint32_t logN, uint64_t ppk, uint32_t L) {
-    if (L < 4 || L >= stop || stop > kTrieMaxStop || logN != stop + 7 || ppk == 0 || ppk > kTrieCap) return false;
+    if (L < 1 || L >= stop || stop > kTrieMaxStop || stop - L > kTrieMaxLevels || logN != stop + 7 || ppk == 0 ||
+        ppk > kTrieCap)
+        return false;
     uint32_t w = 0;
-    for (uint32_t l = L; l <= stop; ++l) w += l >= 5 ? 1u << (l - 5) : 1u;
+    for (uint32_t l = L + 1; l <= stop; ++l) w += trie_words(l);
     return w <= kTrieWords;
 }
-// Batched Eval kernel (dpf_set_eval_kernel): 0 = frontier + per-query walks
-// (default), 1 = the trie kernel where trie_ok holds.  Env DPF_EVAL_TRIE=1
-// sets the initial value.
+// Batched Eval kernel (dpf_set_eval_kernel): 0 = frontier + per-query walks,
+// 1 = the trie kernel where trie_ok holds.  Env DPF_EVAL_TRIE=0|1 sets the
+// initial value.
 static std::atomic<int> g_eval_trie{[] {
     const char* e = getenv("DPF_EVAL_TRIE");
     return e && e[0] == '1' ? 1 : 0;
@@ -999,6 +1007,19 @@ static std::atomic<int> g_eval_trie{[] {
 static bool trie_on() { return g_eval_trie.load(std::memory_order_relaxed) != 0; }
 int set_eval_trie(int on) { return g_eval_trie.exchange(on ? 1 : 0); }
 int get_eval_trie() { return g_eval_trie.load(); }
+
+// The trie kernel's scratch slots (kTrieSlots x 16 KiB = 512 MiB per
+// device, allocated on first use): one slot per hardware workgroup id, so
+// one buffer serves every stream and concurrent launch on the device.
+static void* trie_scratch() {
+    static std::mutex mu;
+    static void* bufs[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!bufs[dev] && hipMalloc(&bufs[dev], kTrieSlots * kTrieCap * 16) != hipSuccess) bufs[dev] = nullptr;
+    return bufs[dev];
+}
 
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
                        uint64_t pts_per_key, uint8_t* out, void* frontier, uint64_t frontier_bytes,
@@ -1022,10 +1043,11 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
         fseed = reinterpret_cast<const uint4*>(fs);
         ft = fts;
     }
-    if (L > 0 && trie_on() && trie_ok(stop, logN, pts_per_key, L)) {
-        const uint64_t blocks = (nkeys + kTrieKeys - 1) / kTrieKeys;
-        hipLaunchKernelGGL(k_eval_trie, dim3((uint32_t)blocks), dim3(kTrieBlock), 0, st, ek, stop, logN, xs, nkeys,
-                           (uint32_t)pts_per_key, fseed, ft, L, out);
+    if (L > 0 && trie_on() && trie_ok(stop, logN, pts_per_key, L) && nq == nkeys * pts_per_key) {
+        uint4* scr = static_cast<uint4*>(trie_scratch());
+        if (scr == nullptr) return hipErrorOutOfMemory;
+        hipLaunchKernelGGL(k_eval_trie, dim3((uint32_t)nkeys), dim3(kTrieBlock), 0, st, ek, stop, logN, xs,
+                           (uint32_t)pts_per_key, fseed, ft, L, scr, out);
         return hipGetLastError();
     }
 #if DPF_EVAL_PAIRS
