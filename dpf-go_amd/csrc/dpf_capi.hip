@@ -681,6 +681,8 @@ int dpf_get_aes_impl(void) { return g_aes_impl.load(); }
 
 int dpf_set_eval_kernel(int kernel) {
     if (kernel != DPF_EVAL_WALK && kernel != DPF_EVAL_TRIE) return fail(DPF_ERR_PARAM, "dpf: unknown Eval kernel");
+    if (kernel == DPF_EVAL_TRIE && !dpfk::eval_trie_built())
+        return fail(DPF_ERR_PARAM, "dpf: the trie Eval kernel is not in this build (make -C dpf-go_amd experimental)");
     return dpfk::set_eval_trie(kernel == DPF_EVAL_TRIE) ? DPF_EVAL_TRIE : DPF_EVAL_WALK;
 }
 

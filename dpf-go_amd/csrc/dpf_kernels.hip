@@ -51,7 +51,7 @@ namespace dpfk {
 
 #ifdef DPF_WAVE_TIMES
 constexpr uint64_t kWaveTimesMax = 1u << 16;
-__device__ uint64_t g_wave_times[4 * kWaveTimesMax];
+__device__ uint64_t g_wave_times[5 * kWaveTimesMax];   // start, end, HW_ID, XCC_ID, walk end
 #endif
 
 struct Ctx {
@@ -365,6 +365,9 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
         CW cw = key_cw<RAW>(c.ks, i);
         walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
+#ifdef DPF_WAVE_TIMES
+    const uint64_t t_walk = wall_clock64();
+#endif
     // Lane pairs share a key when a wave owns one key (UNIFORM): whole-line
     // leaf stores (dfs PAIR).  DPF_PAIR_STORES=0 builds the r02 half-line
     // stores for A/B runs.
@@ -376,10 +379,11 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     if ((threadIdx.x & 63) == 0) {
         const uint64_t wv = u >> 6;
         if (wv < kWaveTimesMax) {
-            g_wave_times[4 * wv] = t_start;
-            g_wave_times[4 * wv + 1] = wall_clock64();
-            g_wave_times[4 * wv + 2] = __builtin_amdgcn_s_getreg(0xF804);   // HW_ID
-            g_wave_times[4 * wv + 3] = __builtin_amdgcn_s_getreg(0xF814);   // XCC_ID
+            g_wave_times[5 * wv] = t_start;
+            g_wave_times[5 * wv + 1] = wall_clock64();
+            g_wave_times[5 * wv + 2] = __builtin_amdgcn_s_getreg(0xF804);   // HW_ID
+            g_wave_times[5 * wv + 3] = __builtin_amdgcn_s_getreg(0xF814);   // XCC_ID
+            g_wave_times[5 * wv + 4] = t_walk;                              // root-to-subtree walk done
         }
     }
 #endif
@@ -453,16 +457,28 @@ struct PairIn {
     uint64_t x0, x1;
     Node n0, n1;
 };
+// UNI: every wave's 64 pairs (128 consecutive queries) belong to one key
+// (pts_per_key a multiple of 128, launch_eval): the key index is wave-uniform,
+// so its correction words come through scalar loads into SGPRs instead of
+// two per-lane copies in VGPRs (12 fewer VGPRs in the walk: the kernel sits
+// at the 128-VGPR limit of 4 waves per SIMD and spilled 35 without it).
+template <bool UNI>
+__device__ __forceinline__ uint64_t pair_key(uint64_t q, uint64_t pts_per_key) {
+    const uint64_t k = q / pts_per_key;
+    if constexpr (UNI) return __builtin_amdgcn_readfirstlane((uint32_t)k);
+    return k;
+}
 // The pair's points and start nodes (frontier gathers): issued before the
 // workgroup fills its table, so their HBM latency overlaps the fill
 // (DPF_EVAL_EARLY; the first pair of every thread).
+template <bool UNI>
 __device__ __forceinline__ PairIn eval_pair_in(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
                                                const uint64_t* __restrict__ xs, uint64_t nq, uint64_t pts_per_key,
                                                const uint4* __restrict__ fseed, const uint8_t* __restrict__ ft,
                                                uint32_t L, uint64_t q0) {
     const uint64_t qa = q0 < nq ? q0 : nq - 1;
     const uint64_t q1 = qa + 1 < nq ? qa + 1 : qa;
-    const uint64_t key0 = qa / pts_per_key, key1 = q1 / pts_per_key;
+    const uint64_t key0 = pair_key<UNI>(qa, pts_per_key), key1 = UNI ? key0 : q1 / pts_per_key;
     const uint64_t rec = (uint64_t)(stop + 2) * 8;
     PairIn p;
     p.x0 = xs[qa];
@@ -471,27 +487,29 @@ __device__ __forceinline__ PairIn eval_pair_in(const uint32_t* __restrict__ ekey
     p.n1 = eval_start(ekeys + key1 * rec, key1, p.x1, logN, fseed, ft, L);
     return p;
 }
+template <bool UNI>
 __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
                                                uint64_t nq, uint64_t pts_per_key, const uint4* __restrict__ fseed,
                                                uint32_t L, uint8_t* __restrict__ out, const uint32_t* s_tab,
                                                uint64_t q0, PairIn p) {
     const bool two = q0 + 1 < nq;
     const uint64_t q1 = two ? q0 + 1 : q0;
-    const uint64_t key0 = q0 / pts_per_key, key1 = q1 / pts_per_key;
+    const uint64_t key0 = pair_key<UNI>(q0, pts_per_key), key1 = UNI ? key0 : q1 / pts_per_key;
     const uint64_t rec = (uint64_t)(stop + 2) * 8;
     const uint32_t* ek0 = ekeys + key0 * rec;
     const uint32_t* ek1 = ekeys + key1 * rec;
     const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
     const uint32_t lo = (threadIdx.x & 31u) * 4u;
     for (uint32_t i = fseed != nullptr ? L : 0; i < stop; ++i) {
-        const CW cw0 = load_cw(ek0, i), cw1 = load_cw(ek1, i);
+        const CW cw0 = load_cw(ek0, i), cw1 = UNI ? cw0 : load_cw(ek1, i);
         walk_step2<DPF_EVAL_BATCH>(tab, lo, p.n0, cw0, path_bit(p.x0, logN - 1 - i), p.n1, cw1,
                                    path_bit(p.x1, logN - 1 - i));
     }
     Blk o0, o1;
     mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, p.n0.s, o0, KeyFixed<false>{}, p.n1.s, o1);
-    o0 = leaf_fix(o0, p.n0.t, load_blk(ek0 + 8 + 8 * stop));
-    o1 = leaf_fix(o1, p.n1.t, load_blk(ek1 + 8 + 8 * stop));
+    const Blk f0 = load_blk(ek0 + 8 + 8 * stop);
+    o0 = leaf_fix(o0, p.n0.t, f0);
+    o1 = leaf_fix(o1, p.n1.t, UNI ? f0 : load_blk(ek1 + 8 + 8 * stop));
     out[q0] = eval_bit(o0, p.x0);
     if (two) out[q1] = eval_bit(o1, p.x1);
 }
@@ -502,6 +520,7 @@ __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekey
 #ifndef DPF_EVAL_PREFETCH
 #define DPF_EVAL_PREFETCH 0   // strided k_eval2: next pair's inputs requested before the current walk (A/B)
 #endif
+template <bool UNI>
 __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                      uint32_t logN, const uint64_t* __restrict__ xs, uint64_t nq,
                                                      uint64_t pts_per_key, const uint4* __restrict__ fseed,
@@ -522,12 +541,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
     // table fill (a short-lived wave otherwise waits out their HBM latency
     // after it).
     PairIn p0{};
-    if (iters) p0 = eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, first);
+    if (iters) p0 = eval_pair_in<UNI>(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, first);
 #endif
     fill_table(s_tab);
     __builtin_amdgcn_s_setprio(3);
 #if DPF_EVAL_EARLY
-    if (iters) eval_pair_walk(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, first, p0);
+    if (iters) eval_pair_walk<UNI>(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, first, p0);
     const uint64_t it0 = 1;
 #else
     const uint64_t it0 = 0;
@@ -536,15 +555,15 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
     // Strided form with the next pair's points and frontier nodes requested
     // before the current pair's walk, so their HBM latency hides under it.
     PairIn nx{};
-    if (it0 < iters) nx = eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, first + it0 * stride);
+    if (it0 < iters) nx = eval_pair_in<UNI>(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, first + it0 * stride);
     for (uint64_t it = it0; it < iters; ++it) {
         if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
         else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
         const uint64_t q0 = first + it * stride;
         const PairIn cur = nx;
-        if (it + 1 < iters) nx = eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0 + stride);
-        eval_pair_walk(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, q0, cur);
+        if (it + 1 < iters) nx = eval_pair_in<UNI>(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0 + stride);
+        eval_pair_walk<UNI>(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, q0, cur);
     }
 #else
     for (uint64_t it = it0; it < iters; ++it) {
@@ -552,12 +571,16 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
         else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
         const uint64_t q0 = first + it * stride;
-        eval_pair_walk(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, q0,
-                       eval_pair_in(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0));
+        eval_pair_walk<UNI>(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, q0,
+                            eval_pair_in<UNI>(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0));
     }
 #endif
 }
 
+#ifndef DPF_EVAL_TRIE_KERNEL
+#define DPF_EVAL_TRIE_KERNEL 0   // k_eval_trie is built only in the experimental build (make experimental)
+#endif
+#if DPF_EVAL_TRIE_KERNEL
 // Batched Eval as a visited-node trie below the frontier.
 // A key's queries share prefixes: at configs[2] (1024 points per key, stop
 // 13) levels 10-13 hold only 647 / 806 / 906 / 963 distinct nodes and 963
@@ -756,6 +779,8 @@ __global__ __launch_bounds__(kTrieBlock, 4) void k_eval_trie(const uint32_t* __r
     }
 }
 
+#endif  // DPF_EVAL_TRIE_KERNEL
+
 // aes128MMO microbenchmark / self-test on the T-table back end: two
 // independent blocks per thread (the PRG's own ILP), iterated `reps` times.
 template <bool RIGHT>
@@ -835,7 +860,7 @@ static uint32_t pick_block(uint64_t n, uint32_t maxb) {
 // Per-thread subtree depth D and workgroup size.  A thread walks span - D
 // levels (one AES each) and expands 3 * 2^D - 2 AES depth-first: deeper
 // subtrees amortise the walk, shallower ones give more, shorter threads.
-// Time model fitted to tools/exp_latency.sh on MI355X (all batch shapes
+// Time model fitted to tools/archive/exp_latency.sh on MI355X (all batch shapes
 // within ~8%): a thread's AES take max(kLat, w * kPerWave) each, w = waves
 // per CU (<= 16; more threads run in further rounds).  The throughput regime
 // (4096 keys x logN=20) takes D = 7; one key at logN=20 takes D = 0, 14 AES
@@ -987,6 +1012,7 @@ uint64_t eval_frontier_bytes(uint64_t nkeys, uint32_t stop, uint64_t pts_per_key
     return ((nkeys << L) * 16 + (nkeys << L) + 255) & ~255ull;
 }
 
+#if DPF_EVAL_TRIE_KERNEL
 // The trie kernel's limits: one key per workgroup, <= 1024 points (2 per
 // thread), every level's bitmap in LDS.
 static bool trie_ok(uint32_t stop, uint32_t logN, uint64_t ppk, uint32_t L) {
@@ -997,17 +1023,6 @@ static bool trie_ok(uint32_t stop, uint32_t logN, uint64_t ppk, uint32_t L) {
     for (uint32_t l = L + 1; l <= stop; ++l) w += trie_words(l);
     return w <= kTrieWords;
 }
-// Batched Eval kernel (dpf_set_eval_kernel): 0 = frontier + per-query walks,
-// 1 = the trie kernel where trie_ok holds.  Env DPF_EVAL_TRIE=0|1 sets the
-// initial value.
-static std::atomic<int> g_eval_trie{[] {
-    const char* e = getenv("DPF_EVAL_TRIE");
-    return e && e[0] == '1' ? 1 : 0;
-}()};
-static bool trie_on() { return g_eval_trie.load(std::memory_order_relaxed) != 0; }
-int set_eval_trie(int on) { return g_eval_trie.exchange(on ? 1 : 0); }
-int get_eval_trie() { return g_eval_trie.load(); }
-
 // The trie kernel's scratch slots (kTrieSlots x 16 KiB = 512 MiB per
 // device, allocated on first use): one slot per hardware workgroup id, so
 // one buffer serves every stream and concurrent launch on the device.
@@ -1020,6 +1035,19 @@ static void* trie_scratch() {
     if (!bufs[dev] && hipMalloc(&bufs[dev], kTrieSlots * kTrieCap * 16) != hipSuccess) bufs[dev] = nullptr;
     return bufs[dev];
 }
+
+#endif
+// Batched Eval kernel (dpf_set_eval_kernel): 0 = frontier + per-query walks,
+// 1 = the trie kernel where trie_ok holds.  Env DPF_EVAL_TRIE=0|1 sets the
+// initial value.
+static std::atomic<int> g_eval_trie{[] {
+    const char* e = getenv("DPF_EVAL_TRIE");
+    return DPF_EVAL_TRIE_KERNEL && e && e[0] == '1' ? 1 : 0;
+}()};
+[[maybe_unused]] static bool trie_on() { return g_eval_trie.load(std::memory_order_relaxed) != 0; }
+int set_eval_trie(int on) { return g_eval_trie.exchange(on ? 1 : 0); }
+bool eval_trie_built() { return DPF_EVAL_TRIE_KERNEL != 0; }
+int get_eval_trie() { return g_eval_trie.load(); }
 
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
                        uint64_t pts_per_key, uint8_t* out, void* frontier, uint64_t frontier_bytes,
@@ -1043,6 +1071,7 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
         fseed = reinterpret_cast<const uint4*>(fs);
         ft = fts;
     }
+#if DPF_EVAL_TRIE_KERNEL
     if (L > 0 && trie_on() && trie_ok(stop, logN, pts_per_key, L) && nq == nkeys * pts_per_key) {
         uint4* scr = static_cast<uint4*>(trie_scratch());
         if (scr == nullptr) return hipErrorOutOfMemory;
@@ -1050,6 +1079,7 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
                            (uint32_t)pts_per_key, fseed, ft, L, scr, out);
         return hipGetLastError();
     }
+#endif
 #if DPF_EVAL_PAIRS
     const uint64_t nthreads = (nq + 1) / 2;
     const uint32_t block = pick_block(nthreads, kBlock);
@@ -1058,8 +1088,17 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
     // strides over the rest.
     const uint64_t resident = 2 * (uint64_t)cu_count();
     if (DPF_EVAL_STRIDE && blocks > resident) blocks = resident;
-    hipLaunchKernelGGL(k_eval2, dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop, logN, xs, nq, pts_per_key,
-                       fseed, ft, L, out);
+    // Wave-uniform keys when every wave's 128 queries share one key.
+    static const bool uni_on = [] {
+        const char* e = getenv("DPF_EVAL_UNIFORM");
+        return !(e && e[0] == '0');
+    }();
+    if (uni_on && pts_per_key % 128 == 0 && block % 64 == 0)
+        hipLaunchKernelGGL(k_eval2<true>, dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop, logN, xs, nq,
+                           pts_per_key, fseed, ft, L, out);
+    else
+        hipLaunchKernelGGL(k_eval2<false>, dim3((uint32_t)blocks), dim3(block), 0, st, ek, stop, logN, xs, nq,
+                           pts_per_key, fseed, ft, L, out);
 #else
     const uint32_t block = pick_block(nq, kBlock);
     const uint64_t blocks = (nq + block - 1) / block;

@@ -57,6 +57,7 @@ uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key);
 // Batched Eval kernel choice: 1 = visited-node trie below the frontier.
 int set_eval_trie(int on);   // returns the previous choice
 int get_eval_trie();
+bool eval_trie_built();   // k_eval_trie is in this build (the experimental one)
 uint64_t eval_frontier_bytes(uint64_t nkeys, uint32_t stop, uint64_t pts_per_key);
 hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const uint64_t* xs, uint64_t nq,
                        uint64_t pts_per_key, uint8_t* out, void* frontier, uint64_t frontier_bytes,

@@ -157,8 +157,24 @@ def test_logN32_dense_oracle_sample():
         assert np.array_equal(np.unpackbits(blk, bitorder="little"), w)
 
 
+def _trie_built() -> bool:
+    try:
+        prev = dpf.set_eval_kernel("trie")
+    except dpf.DPFPanic:
+        return False
+    dpf.set_eval_kernel(prev)
+    return True
+
+
 @pytest.fixture()
 def trie_kernel():
+    """The trie kernel is in the experimental build only (make -C dpf-go_amd
+    experimental; DPF_LIB=dpf-go_amd/lib/variants/libdpf_hip_exp.so)."""
+    if not _trie_built():
+        with pytest.raises(dpf.DPFPanic):
+            dpf.set_eval_kernel("trie")
+        assert dpf.get_eval_kernel() == dpf.EVAL_WALK
+        pytest.skip("k_eval_trie is in the experimental build only")
     prev = dpf.set_eval_kernel("trie")
     yield
     dpf.set_eval_kernel(prev)
