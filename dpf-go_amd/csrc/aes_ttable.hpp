@@ -210,6 +210,64 @@ __device__ __forceinline__ void mmo2(const uint8_t* tab, uint32_t lo, const KA& 
     ob = bxor(b, xb);
 }
 
+// ---- Latency form: one block per quad of lanes (r05) --------------------
+// The serial root-to-subtree walks of small launches run one dependent
+// AES-MMO per level on a nearly idle CU (profiles/r05/wave_times: the walk
+// was half of a 51 us PIR-rank launch at N = 8), so their time is the
+// latency of a round, not the LDS rate.  Here lane j = lane & 3 of a quad
+// holds column j of the state: a round is 3 DPP quad permutes (columns j+1,
+// j+2, j+3), 4 lookups and 3 XOR ops per lane instead of 16 lookups and
+// their address math on one lane.  Round keys are per lane (column j), for
+// the left key and the left^right difference, so a per-quad key select is
+// one v_bitop3 per round.
+struct QuadKeys {
+    uint32_t l[11], d[11];   // rk_L[r][j], (rk_L ^ rk_R)[r][j]; rounds 1..9 pre-rotated by 16
+};
+__device__ __forceinline__ QuadKeys quad_keys(uint32_t j) {
+    QuadKeys k;
+#pragma unroll
+    for (int r = 0; r < 11; ++r) {
+        const uint32_t l0 = dpfc::kRkL.w[4 * r], l1 = dpfc::kRkL.w[4 * r + 1], l2 = dpfc::kRkL.w[4 * r + 2],
+                       l3 = dpfc::kRkL.w[4 * r + 3];
+        const uint32_t d0 = l0 ^ dpfc::kRkR.w[4 * r], d1 = l1 ^ dpfc::kRkR.w[4 * r + 1],
+                       d2 = l2 ^ dpfc::kRkR.w[4 * r + 2], d3 = l3 ^ dpfc::kRkR.w[4 * r + 3];
+        uint32_t l = j == 0 ? l0 : j == 1 ? l1 : j == 2 ? l2 : l3;
+        uint32_t d = j == 0 ? d0 : j == 1 ? d1 : j == 2 ? d2 : d3;
+        if (r >= 1 && r <= 9) {
+            l = rotl(l, 16);
+            d = rotl(d, 16);
+        }
+        k.l[r] = l;
+        k.d[r] = d;
+    }
+    return k;
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+// aes128MMO (aes_amd64.s:51-82) of the quad's block under rk_L ^ (m & d):
+// m = 0 (left key) or ~0 (right key), uniform over the quad.  x = this
+// lane's column of the input; returns its column of the output.
+__device__ __forceinline__ uint32_t mmo_quad(const uint8_t* tab, uint32_t lo, const QuadKeys& k, uint32_t m,
+                                             uint32_t x) {
+    uint32_t s = x ^ k.l[0] ^ (m & k.d[0]);
+#pragma unroll
+    for (int r = 1; r <= 9; ++r) {
+        const uint32_t b = quad_mov<0x39>(s), c = quad_mov<0x4E>(s), d = quad_mov<0x93>(s);   // columns j+1, j+2, j+3
+        const uint32_t ta = tl<0>(tab, s, lo), tb = tl<1, true>(tab, b, lo), tc = tl<2>(tab, c, lo),
+                       td = tl<3, true>(tab, d, lo);
+        const uint32_t rk16 = k.l[r] ^ (m & k.d[r]);
+        s = xor3(ta, tb, rotl(xor3(tc, td, rk16), 16));
+    }
+    const uint32_t b = quad_mov<0x39>(s), c = quad_mov<0x4E>(s), d = quad_mov<0x93>(s);
+    const uint32_t la = tl<0>(tab, s, lo), lb = tl<1>(tab, b, lo), lc = tl<2>(tab, c, lo), ld = tl<3>(tab, d, lo);
+    const uint32_t p = __builtin_amdgcn_perm(lb, la, 0x0c0c0501u);   // {la.b1, lb.b1, 0, 0}
+    const uint32_t q = __builtin_amdgcn_perm(ld, lc, 0x05010c0cu);   // {0, 0, lc.b1, ld.b1}
+    s = __builtin_amdgcn_bitop3_b32(p, q, k.l[10] ^ (m & k.d[10]), kOrXor);
+    return s ^ x;
+}
+
 __device__ __forceinline__ void fill_table(uint32_t* tab) {
     // Row e: 32 copies of Te0[e], then 32 copies of rotl8(Te0[e]); 16-byte stores.
     for (uint32_t i = threadIdx.x; i < 256 * 16; i += blockDim.x) {

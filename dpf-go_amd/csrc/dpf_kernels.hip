@@ -25,6 +25,15 @@
 #ifndef DPF_COOP_WALK
 #define DPF_COOP_WALK 1
 #endif
+#ifndef DPF_QUAD_WALK
+#define DPF_QUAD_WALK 1  // shared walk: one block per quad of lanes on 4 waves (latency form, mmo_quad)
+#endif
+#ifndef DPF_QUAD_FAN
+#define DPF_QUAD_FAN 6   // log2 of the shared walk's paths in the quad form: 6 (4 waves) or 7 (8 waves)
+#endif
+#ifndef DPF_COOP_BFS
+#define DPF_COOP_BFS 0   // 1: the last W - 6 levels of the shared walk breadth-first in LDS (measured slower, r05)
+#endif
 #ifndef DPF_PAIR_STORES
 #define DPF_PAIR_STORES 1
 #endif
@@ -339,26 +348,87 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
         // threads) and leaves them in LDS; every thread then walks only the
         // last W - 6 levels.  Wave-AES per workgroup: l1 + (B/64)(W - 6)
         // instead of (B/64) ltop (configs[4]: 33 vs 96, configs[3]: 39 vs 144).
-        __shared__ uint32_t s_front[64 * 5];
+        //
+        // Breadth-first finish (DPF_COOP_BFS, r05): instead of every thread
+        // walking the last W - 6 levels itself (8 waves x (W - 6) AES, with
+        // paths that share 1/2, 1/4, ... of their nodes), the workgroup
+        // expands the 64 nodes level by level in LDS: step s has 64 * 2^s
+        // parents, one expand (both children, dpf.go:227-240) on each of the
+        // first 2^s waves, so W - 6 = 3 steps are 1 + 2 + 4 wave-expands.  At
+        // the small per-rank shapes the per-thread walk was ~25% of the tree
+        // kernel's AES and ran with all 16 waves of a CU contending for LDS
+        // (tools/wave_times.hip, profiles/r05/wave_times: mean walk 25 us of a
+        // 51 us PIR-rank launch at N = 8).  Node j of step s sits in slot j
+        // (left child 2j, right 2j + 1), so after the last step slot i is
+        // thread i's subtree root.
+        constexpr uint32_t kFs = DPF_COOP_BFS ? kTreeBlock : (1u << (DPF_QUAD_FAN > 6 ? DPF_QUAD_FAN : 6));
+        __shared__ uint32_t s_front[5 * kFs];   // SoA: word k of node j at k * kFs + j
         const uint32_t B = blockDim.x;
         const uint32_t W = 31u - (uint32_t)__builtin_clz(B);
-        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W) {   // uniform over the workgroup
-            const uint32_t l1 = ltop - W + 6;
-            if (threadIdx.x < 64) {
+        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W && B <= (uint32_t)kTreeBlock) {   // uniform
+            // Paths of the shared walk: 2^F, F = 6, or DPF_QUAD_FAN with the
+            // quad form when the workgroup has the 4 * 2^F lanes for it.
+            const uint32_t F = DPF_QUAD_WALK && DPF_QUAD_FAN > 6 && W >= DPF_QUAD_FAN + 2 ? DPF_QUAD_FAN : 6;
+            const uint32_t l1 = ltop - W + F;
+            auto put = [&](uint32_t j, const Node& m) {
+                s_front[j] = m.s.c0; s_front[kFs + j] = m.s.c1; s_front[2 * kFs + j] = m.s.c2;
+                s_front[3 * kFs + j] = m.s.c3; s_front[4 * kFs + j] = m.t;
+            };
+            auto get = [&](uint32_t j) {
+                Node m;
+                m.s = {s_front[j], s_front[kFs + j], s_front[2 * kFs + j], s_front[3 * kFs + j]};
+                m.t = s_front[4 * kFs + j];
+                return m;
+            };
+            if (DPF_QUAD_WALK && W >= 8) {
+                // 2^F paths on the first 2^(F-4) waves, one quad of lanes per
+                // path (the latency form: the walk is serial, the CU nearly idle).
+                if (threadIdx.x < (4u << F)) {
+                    const uint32_t path = threadIdx.x >> 2, j = threadIdx.x & 3u;
+                    const uint64_t subj = (sub - threadIdx.x) + ((uint64_t)path << (W - F));
+                    const QuadKeys qk = quad_keys(j);
+                    uint32_t col = j == 0 ? n.s.c0 : j == 1 ? n.s.c1 : j == 2 ? n.s.c2 : n.s.c3;
+                    uint32_t t = n.t;
+                    for (uint32_t i = 0; i < l1; ++i) {
+                        const CW cw = key_cw<RAW>(c.ks, i);
+                        const uint32_t cwj = j == 0 ? cw.s.c0 : j == 1 ? cw.s.c1 : j == 2 ? cw.s.c2 : cw.s.c3;
+                        walk_step_quad(c.tab, c.lo, qk, j, col, t, cwj, cw.tl, cw.tr,
+                                       (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
+                    }
+                    s_front[j * kFs + path] = col;
+                    if (j == 0) s_front[4 * kFs + path] = t;
+                }
+            } else if (threadIdx.x < 64) {
                 const uint64_t subj = (sub - threadIdx.x) + ((uint64_t)threadIdx.x << (W - 6));
                 Node m = n;
                 for (uint32_t i = 0; i < l1; ++i) {
                     CW cw = key_cw<RAW>(c.ks, i);
                     walk_step<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
                 }
-                uint32_t* f = s_front + 5 * threadIdx.x;
-                f[0] = m.s.c0; f[1] = m.s.c1; f[2] = m.s.c2; f[3] = m.s.c3; f[4] = m.t;
+                put(threadIdx.x, m);
             }
             __syncthreads();
-            const uint32_t* f = s_front + 5 * (threadIdx.x >> (W - 6));
-            n.s = {f[0], f[1], f[2], f[3]};
-            n.t = f[4];
+#if DPF_COOP_BFS
+            for (uint32_t st = 0; st < W - 6; ++st) {
+                const bool act = threadIdx.x < (64u << st);           // the first 2^st waves (uniform per wave)
+                Node m{};
+                if (act) m = get(threadIdx.x);
+                __syncthreads();                                       // every parent read before a child lands
+                if (act) {
+                    const CW cw = key_cw<RAW>(c.ks, l1 + st);
+                    Node L, R;
+                    expand<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, L, R);
+                    put(2 * threadIdx.x, L);
+                    put(2 * threadIdx.x + 1, R);
+                }
+                __syncthreads();
+            }
+            n = get(threadIdx.x);
+            lvl = ltop;
+#else
+            n = get(threadIdx.x >> (W - F));
             lvl = l1;
+#endif
         }
     }
     for (uint32_t i = lvl; i < ltop; ++i) {
@@ -898,8 +968,8 @@ static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes, uint32_t 
         const uint32_t bl = pick_block(threads(d), kTreeBlock);
         const uint32_t W = 31u - (uint32_t)__builtin_clz(bl);
         if (DPF_COOP_WALK && span - d >= 6 && (bl & (bl - 1)) == 0 && W >= 7 && span - d >= W) {
-            walk = (double)(W - 6);
-            lat = (double)(span + prefix_bits - d - W + 6) * kLat;
+            walk = DPF_COOP_BFS ? 0.0 : (double)(W - 6);               // BFS: W - 6 lightly loaded steps instead
+            lat = (double)(span + prefix_bits - d - W + 6 + (DPF_COOP_BFS ? W - 6 : 0)) * kLat;
         }
 #else
         (void)prefix_bits;

@@ -133,6 +133,9 @@ __device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool liv
 #ifndef DPF_FZ_TOUCH
 #define DPF_FZ_TOUCH 1        // k_pir_fused producers touch the next super-group into L2
 #endif
+#ifndef DPF_FOLD_GLDS_DEFAULT
+#define DPF_FOLD_GLDS_DEFAULT 0   // launch_mfma_mt: LDS-DMA fold shape (fold_glds_mode)
+#endif
 #ifndef DPF_FOLD_PRIO
 #define DPF_FOLD_PRIO 1   // issue priority by progress (fold_prio)
 #endif
@@ -924,6 +927,163 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
         }
 }
 
+// ---------------------------------------------------------------------------
+// k_fold_glds: k_fold_mfma with its operands staged by LDS-DMA (r05).
+// PMC on k_fold_mfma<2,2,2,1> at configs[4] (profiles/r05/pmc_fold64): MFMA
+// busy 43% of cycles, TA busy 61-69%, HBM 5.2 TB/s (0.84 of the measured
+// streaming rate), waves waiting on memory 46% of their cycles, 3 waves per
+// SIMD: no unit is saturated; the fold is bound by the bytes it keeps in
+// flight (one staged block of ~20 KiB per workgroup in VGPRs, ~60 KiB per CU
+// against the ~60 KiB that Little's law asks at 6 TB/s and ~2.5 us of loaded
+// latency).  Here global_load_lds_dwordx4 moves every operand straight into
+// a P-deep ring in LDS (no VGPR cost), so P - 1 blocks stay in flight while
+// one is folded; a raw s_barrier plus a counted vmcnt wait per block (never
+// vmcnt(0) in the loop) keeps them in flight across the barrier.
+//   stage = selection rows [kRows][2 SG x 16 B] (XOR-swizzled pieces:
+//           conflict-free ds_read_b128 of a key tile) + each wave's DB
+//           pieces [SG][NT][64 lanes x 16 B];
+//   every wave issues G = 1 + SG * NT LDS-DMAs per block (its share of the
+//   selection rows, then its own DB pieces), so one vmcnt count fits all.
+// Blocks past the end are issued with clamped addresses into the stage that
+// will not be read again, so the count holds to the last block.
+// Only the key-major selection layout (sgm_keys == 0).
+template <int MT, int NT, int SG, int KG, int P>
+struct GldsShape {
+    static constexpr int NS = 8 / NT, NW = NS * KG;
+    static constexpr int kRows = 32 * MT * KG;
+    static constexpr int PR = 2 * SG;                        // 16-byte pieces per selection row
+    static constexpr int kSelPieces = kRows * PR;
+    static constexpr int kSelLanes = kSelPieces / NW;        // per wave (one LDS-DMA, <= 64 lanes)
+    static constexpr int kDbPieces = NW * SG * NT * 64;
+    static constexpr int kStage = kSelPieces + kDbPieces;    // 16-byte slots per stage
+    static constexpr int G = 1 + SG * NT;                    // LDS-DMAs per wave per block
+    static_assert(kSelPieces % NW == 0 && kSelLanes <= 64, "selection rows: one DMA per wave");
+    static_assert(16 % PR == 0, "swizzle: pieces per row divide a bank row");
+};
+template <int PR>
+__device__ __forceinline__ uint32_t sel_slot(uint32_t row, uint32_t q) {
+    constexpr uint32_t rpb = 16 / PR;                        // rows per 256-byte bank row
+    return row * PR + (q ^ ((row / rpb) & (PR - 1)));
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {                  // s_waitcnt vmcnt(N), nothing else
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8)); }
+
+template <int MT, int NT, int SG, int KG, int P>
+__global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
+    const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
+    uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
+    uint32_t par_every) {
+    using Sh = GldsShape<MT, NT, SG, KG, P>;
+    constexpr int NS = Sh::NS, PR = Sh::PR;
+    constexpr bool SC = DPF_FOLD_SEL_CHEAP >= 0 ? DPF_FOLD_SEL_CHEAP == 1 : NT < MT;
+    __shared__ __attribute__((aligned(16))) uint4 s_ring[P * Sh::kStage];   // the only LDS object (glds waits)
+    zero_answers(zero, zero_words);
+    const uint32_t l = threadIdx.x & 63, h = l >> 5, r = l & 31;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = wv % NS, kg = wv / NS;
+    const uint64_t s0 = (uint64_t)blockIdx.x * sg_per_block;
+    const uint64_t s1 = s0 + sg_per_block < nsg ? s0 + sg_per_block : nsg;
+    if (s0 >= s1) return;                                    // uniform over the workgroup
+    const uint64_t nblk = (s1 - s0 + SG - 1) / SG;
+    // Issue block b into stage b % P (clamped past the end).
+    auto issue = [&](uint64_t b) __attribute__((always_inline)) {
+        uint4* st = s_ring + (uint32_t)(b % P) * Sh::kStage;
+        const uint64_t sb = s0 + (b < nblk ? b : nblk - 1) * SG;
+        // selection rows: this wave's kSelLanes slots
+        if (l < (uint32_t)Sh::kSelLanes) {
+            const uint32_t slot = wv * Sh::kSelLanes + l;
+            const uint32_t row = slot / PR, qs = slot % PR;
+            const uint32_t q = qs ^ ((row / (16 / PR)) & (PR - 1));
+            const uint32_t krow = row < nkeys ? row : nkeys - 1;
+            uint64_t word = sb * 8 + 4 * q;
+            if (word + 4 > wpk) word = wpk - 4;
+            __builtin_amdgcn_global_load_lds(bits + (uint64_t)krow * wpk + word, st + wv * Sh::kSelLanes, 16, 0, 0);
+        }
+        // this wave's DB pieces
+#pragma unroll
+        for (int sl = 0; sl < SG; ++sl) {
+            const uint64_t S = sb + sl < s1 ? sb + sl : s1 - 1;
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+                __builtin_amdgcn_global_load_lds(dbs + (S * 256 + 32u * (w * NT + j) + r) * 2 + h,
+                                                 st + Sh::kSelPieces + ((wv * SG + sl) * NT + j) * 64, 16, 0, 0);
+        }
+    };
+    fold_v16f acc[MT][NT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[m][j][e] = 0.0f;
+    uint32_t since = 0;                                      // super-groups since the last parity reduction
+#pragma unroll
+    for (int b = 0; b < P - 1; ++b) issue((uint64_t)b);
+    for (uint64_t b = 0; b < nblk; ++b) {
+        fold_prio(b, nblk);
+        wait_vm<Sh::G * (P - 2)>();                          // this wave's DMAs of block b have landed
+        wait_lgkm0();
+        __builtin_amdgcn_s_barrier();                        // ... and every wave's; block b - 1 fully read
+        issue(b + P - 1);                                    // into the stage block b - 1 used
+        const uint4* st = s_ring + (uint32_t)(b % P) * Sh::kStage;
+        const uint64_t n = s1 - (s0 + b * SG);
+#pragma unroll
+        for (int sl = 0; sl < SG; ++sl) {
+            if ((uint64_t)sl >= n) break;
+            uint4 A[MT], B[NT];
+#pragma unroll
+            for (int m = 0; m < MT; ++m) A[m] = st[sel_slot<PR>(32 * (MT * kg + m) + r, 2 * sl + h)];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) B[j] = st[Sh::kSelPieces + ((wv * SG + sl) * NT + j) * 64 + l];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                fold_v8i bo[NT];
+#pragma unroll
+                for (int j = 0; j < NT; ++j) bo[j] = fp4_db<SC>(u4w(B[j], t));
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    const fold_v8i ao = fp4_sel<SC>(u4w(A[m], t));
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+                        acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ao, bo[j], acc[m][j], kFoldFp4,
+                                                                                   kFoldFp4, 0, kE8M0One, 0, kE8M0One);
+                }
+            }
+        }
+        since += SG;
+        if (since >= par_every) {                            // keep counts below 2^24 (k_fold_mfma)
+            since = 0;
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc[m][j][e] -= 2.0f * __builtin_floorf(acc[m][j][e] * 0.5f);
+        }
+    }
+    wait_vm<0>();                                            // the clamped tail DMAs, before the waves exit
+    constexpr uint32_t pkeys = 32 * MT * KG;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            uint32_t out = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const uint32_t p = ((uint32_t)acc[m][j][e]) & 1u;
+                const uint64_t b = __builtin_amdgcn_ballot_w64(p != 0);
+                const uint32_t row0 = (e & 3) + 8 * (e >> 2);
+                out = l == row0 ? (uint32_t)b : out;
+                out = l == row0 + 4 ? (uint32_t)(b >> 32) : out;
+            }
+            if (l < 32) parts[((uint64_t)blockIdx.x * pkeys + 32 * (MT * kg + m) + l) * 8 + w * NT + j] = out;
+        }
+}
+
 // The sliced layout (above) from a row-major DB of 32-byte records: one wave
 // per 64 records (record groups 2q', 2q'+1 of a super-group); lane l holds
 // record l's 8 words and one ballot per bit position transposes 32 x 32 bits.
@@ -1026,10 +1186,50 @@ hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipSt
 }
 
 namespace {
+template <int MT, int NT, int SG, int KG, int P>
+hipError_t launch_glds(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
+                       uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st) {
+    constexpr int NW = 8 / NT * KG;
+    static int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_glds<MT, NT, SG, KG, P>, 64 * NW, 0) != hipSuccess ||
+            n < 1)
+            n = 1;
+        return n;
+    }();
+    uint64_t spb;
+    split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
+    hipLaunchKernelGGL((k_fold_glds<MT, NT, SG, KG, P>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
+                       reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, fold_par_every());
+    return hipGetLastError();
+}
+
+// DPF_FOLD_GLDS (env; measurement): 0 = register-staged k_fold_mfma, else
+// the LDS-DMA ring k_fold_glds for 33-64 keys: 1 = SG 2, P 4; 2 = SG 2, P 3;
+// 3 = SG 1, P 5; 4 = SG 1, P 6.
+static int fold_glds_mode() {
+    static const int m = [] {
+        const char* e = getenv("DPF_FOLD_GLDS");
+        return e ? atoi(e) : DPF_FOLD_GLDS_DEFAULT;
+    }();
+    return m;
+}
+
 template <int MT, int NT, int SG, int KG>
 hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
                           uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st,
                           uint32_t sgm_keys = 0, uint32_t sgm_g = 1) {
+    if constexpr (MT == 2 && NT == 2 && KG == 1) {
+        if (!sgm_keys) {
+            switch (fold_glds_mode()) {
+                case 1: return launch_glds<2, 2, 2, 1, 4>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
+                case 2: return launch_glds<2, 2, 2, 1, 3>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
+                case 3: return launch_glds<2, 2, 1, 1, 5>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
+                case 4: return launch_glds<2, 2, 1, 1, 6>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
+                default: break;
+            }
+        }
+    }
     constexpr int NW = 8 / NT * KG;
     // Resident workgroups only (one round): each takes a contiguous run of
     // whole staged blocks.  (A fixed 4 workgroups per CU left 1/4 - 3/4 of

@@ -155,6 +155,20 @@ __device__ __forceinline__ void walk_step2(const uint8_t* tab, uint32_t lo, Node
     walk_fix(n1, c1, cw1, bit1);
 }
 
+// walk_step in the quad latency form (aes_ttable.hpp mmo_quad): lane j of the
+// quad holds column j of the node's seed in `col`, and the t byte in `t`
+// (the same on the quad's 4 lanes).  cwj = column j of the level's sCW.
+__device__ __forceinline__ void walk_step_quad(const uint8_t* tab, uint32_t lo, const QuadKeys& k, uint32_t j,
+                                               uint32_t& col, uint32_t& t, uint32_t cwj, uint32_t tl_, uint32_t tr_,
+                                               uint32_t bit) {
+    uint32_t c = mmo_quad(tab, lo, k, bit ? 0xffffffffu : 0u, col);
+    const uint32_t tc = quad_mov<0x00>(c) & 1u;          // getT of column 0 (dpf.go:46-48), on every lane
+    if (j == 0) c &= ~1u;                                // clr (dpf.go:50-52)
+    const uint32_t m = tmask(t);
+    col = c ^ (m & cwj);                                  // dpf.go:185-193
+    t = tc ^ (m & (bit ? tr_ : tl_));
+}
+
 __device__ __forceinline__ void store16(uint8_t* p, Blk v) {
     *reinterpret_cast<uint4*>(p) = make_uint4(v.c0, v.c1, v.c2, v.c3);
 }
