@@ -965,12 +965,45 @@ __device__ __forceinline__ uint32_t sel_slot(uint32_t row, uint32_t q) {
     constexpr uint32_t rpb = 16 / PR;                        // rows per 256-byte bank row
     return row * PR + (q ^ ((row / rpb) & (PR - 1)));
 }
+// The gfx950-only builtins sit behind the device pass: in the host pass
+// clang treats them as invalid in the kernel template's body and silently
+// drops the kernel's host stub (undefined symbol at link time).
 template <int N>
 __device__ __forceinline__ void wait_vm() {                  // s_waitcnt vmcnt(N), nothing else
     static_assert(N >= 0 && N < 64, "vmcnt range");
+#if defined(__HIP_DEVICE_COMPILE__)
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+#endif
 }
-__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8)); }
+__device__ __forceinline__ void wait_lgkm0() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));
+#endif
+}
+// ds_read_b128 hidden from the compiler: an ordinary LDS read of the ring
+// makes hipcc wait vmcnt(0) for every LDS-DMA in flight (it cannot tell the
+// stages apart), which drains the pipeline each block.  The caller waits
+// lgkmcnt(0) (wait_lgkm0) before using the result.
+__device__ __forceinline__ uint4 lds_read16(const uint4* p) {
+    uint4 v;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4*)p;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+#else
+    v = *p;
+#endif
+    return v;
+}
+// global_load_lds_dwordx4: 16 bytes per lane from g to LDS at l + 16 * lane
+// (l wave-uniform).
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+#else
+    (void)g;
+    (void)l;
+#endif
+}
 
 template <int MT, int NT, int SG, int KG, int P>
 __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
@@ -1001,7 +1034,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
             const uint32_t krow = row < nkeys ? row : nkeys - 1;
             uint64_t word = sb * 8 + 4 * q;
             if (word + 4 > wpk) word = wpk - 4;
-            __builtin_amdgcn_global_load_lds(bits + (uint64_t)krow * wpk + word, st + wv * Sh::kSelLanes, 16, 0, 0);
+            glds16(bits + (uint64_t)krow * wpk + word, st + wv * Sh::kSelLanes);
         }
         // this wave's DB pieces
 #pragma unroll
@@ -1009,8 +1042,8 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
             const uint64_t S = sb + sl < s1 ? sb + sl : s1 - 1;
 #pragma unroll
             for (int j = 0; j < NT; ++j)
-                __builtin_amdgcn_global_load_lds(dbs + (S * 256 + 32u * (w * NT + j) + r) * 2 + h,
-                                                 st + Sh::kSelPieces + ((wv * SG + sl) * NT + j) * 64, 16, 0, 0);
+                glds16(dbs + (S * 256 + 32u * (w * NT + j) + r) * 2 + h,
+                       st + Sh::kSelPieces + ((wv * SG + sl) * NT + j) * 64);
         }
     };
     fold_v16f acc[MT][NT];
@@ -1036,9 +1069,10 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
             if ((uint64_t)sl >= n) break;
             uint4 A[MT], B[NT];
 #pragma unroll
-            for (int m = 0; m < MT; ++m) A[m] = st[sel_slot<PR>(32 * (MT * kg + m) + r, 2 * sl + h)];
+            for (int m = 0; m < MT; ++m) A[m] = lds_read16(st + sel_slot<PR>(32 * (MT * kg + m) + r, 2 * sl + h));
 #pragma unroll
-            for (int j = 0; j < NT; ++j) B[j] = st[Sh::kSelPieces + ((wv * SG + sl) * NT + j) * 64 + l];
+            for (int j = 0; j < NT; ++j) B[j] = lds_read16(st + Sh::kSelPieces + ((wv * SG + sl) * NT + j) * 64 + l);
+            wait_lgkm0();
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 fold_v8i bo[NT];

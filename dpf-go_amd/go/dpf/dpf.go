@@ -211,7 +211,8 @@ func SmallCallMaxLogN() uint64 {
 // Batched Eval kernel (include/dpf_hip.h DPF_EVAL_*): EvalWalk (default)
 // walks each query from the shared frontier, EvalTrie computes only the
 // visited nodes of each key's query trie (logN <= 20, <= 1024 points per
-// key; bit-identical, measured slower on MI355X).  Returns the previous one.
+// key; bit-identical, measured slower on MI355X; only in the experimental
+// build, the product library panics on EvalTrie).  Returns the previous one.
 const (
 	EvalWalk = 0
 	EvalTrie = 1
@@ -235,7 +236,8 @@ func GetEvalKernel() int {
 // subtree EvalFull and the matrix-core fold in one launch where it applies
 // (<= 64 keys, logN - prefix_bits = 24..26; measured slower on MI355X),
 // PirFusedAny fuses from logN - prefix_bits = 16 (test mode).  Answers are
-// identical.  Returns the previous one.
+// identical.  The fused kernel is only in the experimental build: the
+// product library panics on PirFused / PirFusedAny.  Returns the previous one.
 const (
 	PirSplit    = 0
 	PirFused    = 1
@@ -253,6 +255,14 @@ func SetPirKernel(kernel int) int {
 // GetPirKernel returns the current PIR kernel setting (dpf_get_pir_kernel).
 func GetPirKernel() int {
 	return int(C.dpf_get_pir_kernel())
+}
+
+// SetFoldLimits caps the workgroups of a fold launch and sets how many
+// 256-record super-groups the matrix-core fold accumulates between parity
+// reductions (dpf_set_fold_limits; 0 = default).  Answers do not depend on
+// either: tuning and tests only.
+func SetFoldLimits(maxBlocks uint32, parityEvery uint32) {
+	check(C.dpf_set_fold_limits(C.uint32_t(maxBlocks), C.uint32_t(parityEvery)))
 }
 
 // PirKernelFor reports which kernel a PIR answer of this shape runs now

@@ -155,8 +155,11 @@ int dpf_get_aes_impl(void);
  * DPF_EVAL_TRIE: the same frontier, then only the visited nodes of each
  * key's query trie below it (5,307 instead of 6,142 AES per
  * key at configs[2]), where logN <= 20 and pts_per_key <= 1024; the walk
- * kernel elsewhere.  Outputs are bit-identical.  Process-wide; env
- * DPF_EVAL_TRIE=1 sets the initial value. */
+ * kernel elsewhere.  Outputs are bit-identical.  The trie kernel was
+ * measured slower and is built only in the experimental library (make
+ * -C dpf-go_amd experimental); the product library returns DPF_ERR_PARAM
+ * for DPF_EVAL_TRIE.  Process-wide; env DPF_EVAL_TRIE=1 sets the initial
+ * value (experimental build). */
 #define DPF_EVAL_WALK 0
 #define DPF_EVAL_TRIE 1
 int dpf_set_eval_kernel(int kernel);   /* returns the previous kernel */
@@ -268,8 +271,10 @@ int dpf_set_fold_limits(uint32_t max_blocks, uint32_t parity_every);
  * lane and 4 waves fold each leaf pair from LDS), so the selection bits
  * never reach HBM; measured slower on MI355X, the split
  * path elsewhere.  DPF_PIR_FUSED_ANY fuses any slice from logN -
- * prefix_bits = 16 (test mode).  Answers are identical.  Process-wide; env
- * DPF_PIR_KERNEL=split|fused|fused-any. */
+ * prefix_bits = 16 (test mode).  Answers are identical.  The fused kernel is
+ * built only in the experimental library (make -C dpf-go_amd experimental):
+ * the product library returns DPF_ERR_PARAM for DPF_PIR_FUSED and
+ * DPF_PIR_FUSED_ANY.  Process-wide; env DPF_PIR_KERNEL=split|fused|fused-any. */
 #define DPF_PIR_SPLIT 0
 #define DPF_PIR_FUSED 1
 #define DPF_PIR_FUSED_ANY 2
