@@ -509,7 +509,18 @@ __global__ __launch_bounds__(256) void k_xor_parts(const uint32_t* __restrict__ 
     if (t >= nkeys * pwords) return;
     const uint32_t k = t / pwords, i = t % pwords;
     uint32_t v = 0;
-    for (uint64_t p = blockIdx.y; p < nparts; p += gridDim.y) v ^= parts[(p * pkeys + k) * pwords + i];
+    // Eight independent loads in flight per step (a strided loop of single
+    // loads left the kernel at ~5 us, mostly dependent L2 round trips).
+    const uint64_t g = gridDim.y;
+    uint64_t p = blockIdx.y;
+    for (; p + 7 * g < nparts; p += 8 * g) {
+        uint32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = parts[((p + u * g) * pkeys + k) * pwords + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v ^= x[u];
+    }
+    for (; p < nparts; p += g) v ^= parts[(p * pkeys + k) * pwords + i];
     if (v) atomicXor(ans + (uint64_t)k * ans_words + off + i, v);
 }
 
@@ -982,17 +993,28 @@ __device__ __forceinline__ void wait_lgkm0() {
 }
 // ds_read_b128 hidden from the compiler: an ordinary LDS read of the ring
 // makes hipcc wait vmcnt(0) for every LDS-DMA in flight (it cannot tell the
-// stages apart), which drains the pipeline each block.  The caller waits
-// lgkmcnt(0) (wait_lgkm0) before using the result.
-__device__ __forceinline__ uint4 lds_read16(const uint4* p) {
-    uint4 v;
+// stages apart), which drains the pipeline each block.  The caller passes
+// the results through lgkm_ready() before using them: the compiler sees no
+// dependence between the asm load and a plain s_waitcnt, and would hoist
+// the uses above the wait.
+typedef uint32_t fold_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ fold_u4 lds_read16(const uint4* p) {
+    fold_u4 v;
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4*)p;
     asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
 #else
-    v = *p;
+    v = fold_u4{p->x, p->y, p->z, p->w};
 #endif
     return v;
+}
+// s_waitcnt lgkmcnt(0) tied to v: uses of v stay below the wait.
+__device__ __forceinline__ void lgkm_ready(fold_u4& v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v));
+#else
+    (void)v;
+#endif
 }
 // global_load_lds_dwordx4: 16 bytes per lane from g to LDS at l + 16 * lane
 // (l wave-uniform).
@@ -1067,20 +1089,23 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
 #pragma unroll
         for (int sl = 0; sl < SG; ++sl) {
             if ((uint64_t)sl >= n) break;
-            uint4 A[MT], B[NT];
+            fold_u4 A[MT], B[NT];
 #pragma unroll
             for (int m = 0; m < MT; ++m) A[m] = lds_read16(st + sel_slot<PR>(32 * (MT * kg + m) + r, 2 * sl + h));
 #pragma unroll
             for (int j = 0; j < NT; ++j) B[j] = lds_read16(st + Sh::kSelPieces + ((wv * SG + sl) * NT + j) * 64 + l);
-            wait_lgkm0();
+#pragma unroll
+            for (int m = 0; m < MT; ++m) lgkm_ready(A[m]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) lgkm_ready(B[j]);
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 fold_v8i bo[NT];
 #pragma unroll
-                for (int j = 0; j < NT; ++j) bo[j] = fp4_db<SC>(u4w(B[j], t));
+                for (int j = 0; j < NT; ++j) bo[j] = fp4_db<SC>(B[j][t]);
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
-                    const fold_v8i ao = fp4_sel<SC>(u4w(A[m], t));
+                    const fold_v8i ao = fp4_sel<SC>(A[m][t]);
 #pragma unroll
                     for (int j = 0; j < NT; ++j)
                         acc[m][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ao, bo[j], acc[m][j], kFoldFp4,

@@ -51,6 +51,11 @@ def main():
         res["eval"][str(logN)] = erow
     dpf.set_small_call_path("auto")
     res["auto_max_logN"] = dpf.small_call_max_logN()
+    res["host_isa"] = os.environ.get("DPF_HOST_ISA", "auto")
+    # Largest logN whose host EvalFull beats the GPU round trip (the AUTO
+    # threshold this host ISA should have).
+    wins = [int(n) for n, r in res["evalfull"].items() if r["host_ms"] < r["gpu_ms"]]
+    res["measured_crossover_logN"] = max(wins) if wins else None
     print(json.dumps(res))
 
 
