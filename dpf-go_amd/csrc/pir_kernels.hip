@@ -133,6 +133,9 @@ __device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool liv
 #ifndef DPF_FZ_TOUCH
 #define DPF_FZ_TOUCH 1        // k_pir_fused producers touch the next super-group into L2
 #endif
+#ifndef DPF_FOLD_ABLATE
+#define DPF_FOLD_ABLATE 0   // measurement builds of k_fold_mfma: 1 = loads only, 2 = no HBM reads (wrong answers)
+#endif
 #ifndef DPF_FOLD_GLDS_DEFAULT
 #define DPF_FOLD_GLDS_DEFAULT 0   // launch_mfma_mt: LDS-DMA fold shape (fold_glds_mode)
 #endif
@@ -797,7 +800,12 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
             const uint64_t S = sb + q / 2;
             const uint64_t at = SGM ? ((S / SGM * sgm_keys + row) * SGM + S % SGM) * 8 + 4 * (q & 1)
                                     : (uint64_t)row * wpk + word;
+#if DPF_FOLD_ABLATE == 2
+            const uint32_t z = (uint32_t)at * 2654435761u;      // no HBM read (measurement build)
+            const uint4 x = make_uint4(z, z ^ 0x5555u, z + 7u, ~z);
+#else
             const uint4 x = *reinterpret_cast<const uint4*>(bits + (ok ? at : 0));
+#endif
             v[i] = ok ? x : make_uint4(0, 0, 0, 0);
         }
     };
@@ -816,7 +824,14 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
         for (int sl = 0; sl < SG; ++sl) {
             const uint64_t S = sb + sl < s1 ? sb + sl : s1 - 1;
 #pragma unroll
-            for (int j = 0; j < NT; ++j) B[sl][j] = dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h];
+            for (int j = 0; j < NT; ++j) {
+#if DPF_FOLD_ABLATE == 2
+                const uint32_t z = (uint32_t)((S * 256 + 32u * (w * NT + j) + r) * 2 + h) * 2246822519u;
+                B[sl][j] = make_uint4(z, z + 1u, z ^ 0xAAAAu, ~z);           // no HBM read (measurement build)
+#else
+                B[sl][j] = dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h];
+#endif
+            }
         }
     };
     fold_v16f acc[MT][NT];
@@ -842,6 +857,19 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
 #pragma unroll
         for (int m = 0; m < MT; ++m)
             A[m] = *reinterpret_cast<const uint4*>(&s_sel[(32 * (MT * kg + m) + r) * kRow + 8 * sl + 4 * h]);
+#if DPF_FOLD_ABLATE == 1
+        // Measurement build: the operands are consumed by one XOR each, no
+        // FP4 expansion and no MFMA (the load + staging structure alone).
+        uint32_t x = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) x ^= u4w(B[j], t);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) x ^= u4w(A[m], t);
+        }
+        acc[0][0][0] += (float)(x & 1u);
+#else
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             fold_v8i bo[NT];
@@ -856,6 +884,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
                                                                                0, kE8M0One, 0, kE8M0One);
             }
         }
+#endif
     };
 #if DPF_FOLD_PD >= 2
     // Two blocks in flight: block i folds from buffer i%3 while blocks i+1
@@ -938,6 +967,10 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
         }
 }
 
+#ifndef DPF_FOLD_GLDS_KERNEL
+#define DPF_FOLD_GLDS_KERNEL 0   // k_fold_glds: experimental build only (measured slower, r05)
+#endif
+#if DPF_FOLD_GLDS_KERNEL
 // ---------------------------------------------------------------------------
 // k_fold_glds: k_fold_mfma with its operands staged by LDS-DMA (r05).
 // PMC on k_fold_mfma<2,2,2,1> at configs[4] (profiles/r05/pmc_fold64): MFMA
@@ -1143,6 +1176,8 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
         }
 }
 
+#endif  // DPF_FOLD_GLDS_KERNEL
+
 // The sliced layout (above) from a row-major DB of 32-byte records: one wave
 // per 64 records (record groups 2q', 2q'+1 of a super-group); lane l holds
 // record l's 8 words and one ballot per bit position transposes 32 x 32 bits.
@@ -1245,6 +1280,7 @@ hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipSt
 }
 
 namespace {
+#if DPF_FOLD_GLDS_KERNEL
 template <int MT, int NT, int SG, int KG, int P>
 hipError_t launch_glds(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
                        uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st) {
@@ -1274,10 +1310,13 @@ static int fold_glds_mode() {
     return m;
 }
 
+#endif
+
 template <int MT, int NT, int SG, int KG>
 hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
                           uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st,
                           uint32_t sgm_keys = 0, uint32_t sgm_g = 1) {
+#if DPF_FOLD_GLDS_KERNEL
     if constexpr (MT == 2 && NT == 2 && KG == 1) {
         if (!sgm_keys) {
             switch (fold_glds_mode()) {
@@ -1289,6 +1328,7 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
             }
         }
     }
+#endif
     constexpr int NW = 8 / NT * KG;
     // Resident workgroups only (one round): each takes a contiguous run of
     // whole staged blocks.  (A fixed 4 workgroups per CU left 1/4 - 3/4 of
