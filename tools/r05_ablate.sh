@@ -13,7 +13,9 @@ export FOLD_MODE=mfma
 for r in 1 2 3; do
   for b in fold_bench bin/fold_bench_ablate1 bin/fold_bench_ablate2; do
     for lg in 24 21; do
-      timeout -k 10 60 tools/$b 64 32 $lg > "$OUT/ab.json" 2>&1 || { echo "$b failed"; cat "$OUT/ab.json"; exit 1; }
+      timeout -k 10 60 tools/$b 64 32 $lg > "$OUT/ab.json" 2>&1
+      rc=$?   # the ablation builds compute wrong answers on purpose: fold_bench exits 1 ("ok": false)
+      if [ $rc -ne 0 ] && ! grep -q '"fold_us"' "$OUT/ab.json"; then echo "$b failed rc=$rc"; cat "$OUT/ab.json"; exit 1; fi
       python3 -c "import json; d=json.load(open('$OUT/ab.json')); print('$r $(basename $b) logN=$lg', d['fold_us'], 'us', d['GBs'], 'GB/s')" | tee -a "$OUT/ablate.txt"
     done
   done
