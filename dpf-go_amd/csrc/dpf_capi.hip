@@ -784,13 +784,14 @@ std::atomic<int> g_small_mode{[] {
 // Largest logN whose single-key EvalFull goes to the host in AUTO mode: up
 // to it, one key's host EvalFull (3*2^(logN-7) AES on VAES) is faster than
 // the GPU round trip (key H2D, launch, output D2H, sync) -- measured on the
-// GPU box's EPYC (profiles/r03/small_calls).
+// GPU box's EPYC (profiles/r03/small_calls; r05: host 69 us vs GPU 89 us at
+// 21, 137 vs 105 at 22, profiles/r05/small_calls/small_vaes.json).
 constexpr uint32_t kSmallFullMaxLogN = 21;
-// Without VAES the host EvalFull runs 1 block per AESENC instead of 4 (two
-// 128-bit chains per node), ~3x slower at these sizes: at logN = 20 ~92 us
-// against the GPU's 80.7, at 19 ~45 against ~65.  An estimate from the
-// VAES / AES-NI ratio of the host kernels, not a separate measurement.
-constexpr uint32_t kSmallFullMaxLogNNoVaes = 19;
+// Without VAES (DPF_HOST_ISA=aesni: two 128-bit AES-NI chains per node) the
+// host path is ~2x slower at these sizes; measured crossover logN = 20: host
+// 72 us vs GPU 83 us at 20, 138 vs 100 at 21
+// (profiles/r05/small_calls/small_aesni.json; r04's 19 was an estimate).
+constexpr uint32_t kSmallFullMaxLogNNoVaes = 20;
 // DPF_SMALL_HOST's ceiling: two host-side levels of the full width (~2.1x the
 // output) and one core; above it the call goes to the GPU.
 constexpr uint32_t kHostFullMaxLogN = 28;

@@ -81,6 +81,24 @@ __device__ __forceinline__ void fold_prio(uint64_t done, uint64_t all) {
     (void)all;
 #endif
 }
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup
+// fence on all memory plus s_barrier, and its fence waits vmcnt(0): every
+// global load in flight -- the next block's operands, prefetched across the
+// barrier on purpose -- must land before any wave passes.  The folds only
+// need their LDS staging ordered, so this fences the local address space
+// (lgkmcnt) and leaves the prefetch in flight (r05, DPF_FOLD_RAW_BARRIER).
+#ifndef DPF_FOLD_RAW_BARRIER
+#define DPF_FOLD_RAW_BARRIER 1
+#endif
+__device__ __forceinline__ void lds_barrier() {
+#if DPF_FOLD_RAW_BARRIER
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#else
+    __syncthreads();
+#endif
+}
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -451,14 +469,14 @@ __global__ __launch_bounds__(64 * WV, WV == 8 ? 4 : 3) void k_fold4r(const uint3
     };
     for (uint64_t cb = c0; cb < cend; cb += Cfg::batch) {
         fold_prio(cb - c0, cend - c0);
-        __syncthreads();                                   // previous batch's selection reads are done
+        lds_barrier();                                     // previous batch's selection reads are done
 #pragma unroll
         for (int kg = 0; kg < KW; ++kg) {
             uint32_t* row = &s_sel[(kg * 64 + sk) * Cfg::sel_row + 4 * sp];
             *reinterpret_cast<uint2*>(row) = make_uint2(snext[kg].x, snext[kg].y);
             *reinterpret_cast<uint2*>(row + 2) = make_uint2(snext[kg].z, snext[kg].w);
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int kg = 0; kg < KW; ++kg) snext[kg] = load_sel(kg, cb + Cfg::batch);
 #pragma unroll
@@ -898,9 +916,9 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
     auto block = [&](uint64_t sb, const uint4 (&Bc)[SG][NT], uint4 (&Bf)[SG][NT], const uint4 (&svc)[kPer],
                      uint4 (&svf)[kPer]) __attribute__((always_inline)) {
         fold_prio(sb - s0, s1 - s0);
-        __syncthreads();                                        // previous block's operand reads are done
+        lds_barrier();                                          // previous block's operand reads are done
         store_sel(svc);
-        __syncthreads();
+        lds_barrier();
         const uint64_t nb = sb + 2 * SG < s1 ? sb + 2 * SG : sb;   // block after next (clamped)
         load_sel(nb, svf);
         load_db(nb, Bf);
@@ -928,9 +946,9 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
     // issued, then its super-groups folded.
     auto block = [&](uint64_t sb, const uint4 (&Bc)[SG][NT], uint4 (&Bn)[SG][NT]) __attribute__((always_inline)) {
         fold_prio(sb - s0, s1 - s0);
-        __syncthreads();                                        // previous block's operand reads are done
+        lds_barrier();                                          // previous block's operand reads are done
         store_sel(sv);
-        __syncthreads();
+        lds_barrier();
         const uint64_t nb = sb + SG < s1 ? sb + SG : sb;        // next block (clamped)
         load_sel(nb, sv);
         load_db(nb, Bn);

@@ -170,7 +170,7 @@ int dpf_get_eval_kernel(void);
  * AES units (host_eval.cpp: AES-NI/VAES, bit-exact with the kernels) when
  * that beats a GPU round trip: every dpf_eval, and dpf_evalfull up to
  * logN = dpf_small_call_max_logN(), which depends on the host (21 with
- * VAES, 19 with AES-NI only); DPF_SMALL_GPU always uses the GPU,
+ * VAES, 20 with AES-NI only); DPF_SMALL_GPU always uses the GPU,
  * DPF_SMALL_HOST the host whenever it has AES-NI, except dpf_evalfull above
  * logN = 28 (outputs of 32 MiB and more), which stays on the GPU.  Either
  * way a gfx950

@@ -316,3 +316,37 @@ def test_host_path_exactness_rules(host_shim, logN):
         assert np.array_equal(_host_full(host_shim, k, logN), oracle.evalfull_batch(k, logN))
         xs = synth.eval_points(1, 64, logN)
         assert np.array_equal(_host_eval(host_shim, k, xs, logN), oracle.eval_batch(k, xs, logN))
+
+
+def test_small_call_thresholds_match_the_recorded_crossovers():
+    """the AUTO routing threshold of each host ISA is the largest
+    logN at which the host EvalFull measured faster than the GPU round trip
+    on the GPU box (tools/small_calls.py -> profiles/r05/small_calls), for
+    VAES and for AES-NI only (DPF_HOST_ISA=aesni).  Checked against the
+    recorded medians rather than a wall-clock race in the test, which the
+    box's load would decide."""
+    import subprocess
+    import sys
+    prof = os.path.join(ROOT, "profiles", "r05", "small_calls")
+    flags = set()
+    for ln in open("/proc/cpuinfo"):
+        if ln.startswith("flags"):
+            flags = set(ln.split(":", 1)[1].split())
+            break
+    if "aes" not in flags:
+        pytest.skip("host without AES-NI")
+    code = "import sys; sys.path.insert(0, %r); import dpf; print(dpf.small_call_max_logN())" % os.path.join(
+        ROOT, "dpf-go_amd")
+    for isa, name in (("aesni", "small_aesni.json"), ("auto", "small_vaes.json")):
+        if isa == "auto" and not {"vaes", "avx512f"} <= flags:
+            continue                                   # this CPU would take the AES-NI path
+        rec = json.load(open(os.path.join(prof, name)))
+        wins = sorted(int(n) for n, r in rec["evalfull"].items() if r["host_ms"] < r["gpu_ms"])
+        losses = sorted(int(n) for n, r in rec["evalfull"].items() if r["host_ms"] >= r["gpu_ms"])
+        assert wins and losses and max(wins) < min(losses), rec["evalfull"]
+        env = dict(os.environ)
+        env.pop("DPF_HOST_ISA", None)
+        if isa == "aesni":
+            env["DPF_HOST_ISA"] = "aesni"
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+        assert int(out.stdout.strip().splitlines()[-1]) == max(wins), (isa, out.stdout, max(wins))

@@ -56,8 +56,10 @@ def test_short_key_still_panics_like_the_reference():
 def test_auto_mode_is_faster_than_the_gpu_round_trip_where_it_routes():
     """Loose sanity of the threshold: at logN = small_call_max_logN() the
     host call is not far slower than the GPU round trip (median of 15).  The
-    threshold itself is measured by tools/small_calls.py; a tight wall-clock
-    ratio here would be at the mercy of host load and GPU clocks."""
+    threshold itself is measured by tools/small_calls.py for both host ISAs,
+    and the CPU test test_capi.py::test_small_call_thresholds_match_the_
+    recorded_crossovers holds the library to those measurements; a tight
+    wall-clock ratio here would be at the mercy of host load and GPU clocks."""
     logN = dpf.small_call_max_logN()
     al, s0, s1 = synth.key_seeds(1, logN, first=9)
     ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
