@@ -1138,8 +1138,8 @@ int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_strid
 
 size_t dpf_xor_fold_workspace_size(void) { return dpfk::pir_fold_parts_bytes(); }
 
-int dpf_set_fold_limits(uint32_t max_blocks, uint32_t parity_every) {
-    dpfk::set_fold_limits(max_blocks, parity_every);
+int dpf_set_fold_limits(uint32_t max_blocks, uint32_t max_sg_per_block) {
+    dpfk::set_fold_limits(max_blocks, max_sg_per_block);
     return DPF_OK;
 }
 

@@ -555,18 +555,18 @@ static int cu_count_fold() {
 
 constexpr uint64_t kFoldMaxBlocks = 1024;          // workgroups per launch (partials area)
 constexpr uint64_t kFoldPartBytes = 64 * 4 * 32 * 2;   // largest part: 64*KW keys x 32C bytes, KW*C <= 8
-constexpr uint32_t kFoldParEveryMax = 1u << 15;    // k_fold_mfma: super-groups between parity reductions
+constexpr uint32_t kFoldMaxSgPerBlock = 1u << 15; // k_fold_mfma: super-groups per workgroup (fp32-exact counts)
 
 uint64_t pir_fold_parts_bytes() { return kFoldMaxBlocks * kFoldPartBytes; }
 
-// Tuning / test limits (set_fold_limits): workgroups per fold launch and the
-// MFMA fold's parity-reduction period.
+// Tuning / test limits (set_fold_limits): workgroups per fold launch and
+// super-groups per matrix-core fold workgroup.
 static std::atomic<uint32_t> g_fold_blocks{(uint32_t)kFoldMaxBlocks};
-static std::atomic<uint32_t> g_fold_par_every{kFoldParEveryMax};
-static uint32_t fold_par_every() { return g_fold_par_every.load(std::memory_order_relaxed); }
-void set_fold_limits(uint32_t max_blocks, uint32_t par_every) {
+static std::atomic<uint32_t> g_fold_max_sg{kFoldMaxSgPerBlock};
+static uint32_t fold_max_sg() { return g_fold_max_sg.load(std::memory_order_relaxed); }
+void set_fold_limits(uint32_t max_blocks, uint32_t max_sg) {
     g_fold_blocks.store(max_blocks == 0 || max_blocks > kFoldMaxBlocks ? (uint32_t)kFoldMaxBlocks : max_blocks);
-    g_fold_par_every.store(par_every == 0 || par_every > kFoldParEveryMax ? kFoldParEveryMax : par_every);
+    g_fold_max_sg.store(max_sg == 0 || max_sg > kFoldMaxSgPerBlock ? kFoldMaxSgPerBlock : max_sg);
 }
 
 namespace {
@@ -769,17 +769,20 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 // of a key per chunk, as the PIR tree kernel writes them), so a staged block
 // is one contiguous region instead of EvalFull's key-major [key][wpk words].
 // Exactness of the fp32 counts: an accumulator gains at most 64 per MFMA
-// (one per record of a K-block), and fp32 holds every integer up to 2^24.  A
-// wave's run of super-groups is unbounded (sg_per_block grows with the DB and
-// shrinks with the CU count), so every `par_every` super-groups (<=
-// kFoldParEveryMax = 2^15, i.e. 2^23 records) the accumulators are reduced to
-// their parities: count - 2 floor(count / 2), exact below 2^24.  Between two
-// reductions a count stays below (2^15 + 3 SG) * 256 < 2^24.
+// (one per record of a K-block), and fp32 holds every integer up to 2^24.
+// A workgroup's run of super-groups would grow with the DB and shrink with
+// the CU count, so launch_mfma_mt never gives one more than
+// kFoldMaxSgPerBlock = 2^15 super-groups (2^23 records): it adds workgroups,
+// and beyond kFoldMaxBlocks of them it folds the DB in passes, each pass's
+// partials XORed into the answers.  (Reducing the counts to parities inside
+// the kernel moved the large-tile accumulators out of AGPRs and spilled them:
+// 2.5x slower at 256 keys, r05.)  wlim: selection words per key row from
+// `bits` (the row stride stays wpk), so a pass can start mid-row.
 template <int MT, int NT, int SG, int KG, int SGM = 0>
 __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
-    uint32_t par_every, uint32_t sgm_keys = 0) {
+    uint64_t wlim, uint32_t sgm_keys = 0) {
     constexpr int NS = 8 / NT;                                 // bit slices
     constexpr int NW = NS * KG;
     constexpr bool SC = DPF_FOLD_SEL_CHEAP >= 0 ? DPF_FOLD_SEL_CHEAP == 1 : NT < MT;
@@ -814,7 +817,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
             uint32_t row, q;
             piece(p, row, q);
             const uint64_t word = sb * 8 + 4 * q;
-            const bool ok = p < (uint32_t)kPieces && row < nkeys && word + 4 <= wpk;
+            const bool ok = p < (uint32_t)kPieces && row < nkeys && word + 4 <= wlim;
             const uint64_t S = sb + q / 2;
             const uint64_t at = SGM ? ((S / SGM * sgm_keys + row) * SGM + S % SGM) * 8 + 4 * (q & 1)
                                     : (uint64_t)row * wpk + word;
@@ -859,16 +862,6 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[m][j][e] = 0.0f;
-    uint32_t since = 0;                                        // super-groups since the last parity reduction
-    auto to_parity = [&]() __attribute__((always_inline)) {
-        since = 0;
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int j = 0; j < NT; ++j)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc[m][j][e] -= 2.0f * __builtin_floorf(acc[m][j][e] * 0.5f);
-    };
     // One super-group: 4 K-blocks of 64 records x MT x NT MFMAs.
     auto fold_sg = [&](int sl, const uint4 (&B)[NT]) __attribute__((always_inline)) {
         uint4 A[MT];
@@ -926,8 +919,6 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
 #pragma unroll
         for (int sl = 0; sl < SG; ++sl)
             if ((uint64_t)sl < n) fold_sg(sl, Bc[sl]);
-        since += SG;
-        if (since >= par_every) to_parity();                   // uniform
     };
     uint64_t sb = s0;
     for (; sb + 2 * SG < s1; sb += 3 * SG) {
@@ -956,8 +947,6 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
 #pragma unroll
         for (int sl = 0; sl < SG; ++sl)
             if ((uint64_t)sl < n) fold_sg(sl, Bc[sl]);
-        since += SG;
-        if (since >= par_every) to_parity();                   // uniform
     };
     uint64_t sb = s0;
     for (; sb + SG < s1; sb += 2 * SG) {
@@ -1082,7 +1071,7 @@ template <int MT, int NT, int SG, int KG, int P>
 __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
-    uint32_t par_every) {
+    uint64_t wlim) {
     using Sh = GldsShape<MT, NT, SG, KG, P>;
     constexpr int NS = Sh::NS, PR = Sh::PR;
     constexpr bool SC = DPF_FOLD_SEL_CHEAP >= 0 ? DPF_FOLD_SEL_CHEAP == 1 : NT < MT;
@@ -1106,7 +1095,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
             const uint32_t q = qs ^ ((row / (16 / PR)) & (PR - 1));
             const uint32_t krow = row < nkeys ? row : nkeys - 1;
             uint64_t word = sb * 8 + 4 * q;
-            if (word + 4 > wpk) word = wpk - 4;
+            if (word + 4 > wlim) word = wlim - 4;
             glds16(bits + (uint64_t)krow * wpk + word, st + wv * Sh::kSelLanes);
         }
         // this wave's DB pieces
@@ -1126,7 +1115,6 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
         for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[m][j][e] = 0.0f;
-    uint32_t since = 0;                                      // super-groups since the last parity reduction
 #pragma unroll
     for (int b = 0; b < P - 1; ++b) issue((uint64_t)b);
     for (uint64_t b = 0; b < nblk; ++b) {
@@ -1163,16 +1151,6 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, 2) void k_fold_glds(
                                                                                    kFoldFp4, 0, kE8M0One, 0, kE8M0One);
                 }
             }
-        }
-        since += SG;
-        if (since >= par_every) {                            // keep counts below 2^24 (k_fold_mfma)
-            since = 0;
-#pragma unroll
-            for (int m = 0; m < MT; ++m)
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[m][j][e] -= 2.0f * __builtin_floorf(acc[m][j][e] * 0.5f);
         }
     }
     wait_vm<0>();                                            // the clamped tail DMAs, before the waves exit
@@ -1300,20 +1278,14 @@ hipError_t launch_slice_db(const uint8_t* db, uint64_t nrec, uint8_t* dbs, hipSt
 namespace {
 #if DPF_FOLD_GLDS_KERNEL
 template <int MT, int NT, int SG, int KG, int P>
-hipError_t launch_glds(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
-                       uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st) {
+hipError_t launch_glds(const uint32_t* bits, uint64_t wpk, uint64_t wlim, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
+                       uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t want, uint64_t& blocks,
+                       hipStream_t st) {
     constexpr int NW = 8 / NT * KG;
-    static int per_cu = [] {
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_glds<MT, NT, SG, KG, P>, 64 * NW, 0) != hipSuccess ||
-            n < 1)
-            n = 1;
-        return n;
-    }();
     uint64_t spb;
-    split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
+    split_chunks(nsg, want, SG, blocks, spb);
     hipLaunchKernelGGL((k_fold_glds<MT, NT, SG, KG, P>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                       reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, fold_par_every());
+                       reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, wlim);
     return hipGetLastError();
 }
 
@@ -1330,23 +1302,14 @@ static int fold_glds_mode() {
 
 #endif
 
+// One key group (<= 32 * MT * KG keys) over the sliced DB: passes of at most
+// (workgroup cap) x kFoldMaxSgPerBlock super-groups, each a fold launch whose
+// workgroups fold <= kFoldMaxSgPerBlock super-groups (fp32-exact counts, see
+// k_fold_mfma) and a k_xor_parts launch that XORs the partials into ans.
 template <int MT, int NT, int SG, int KG>
 hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs, uint64_t nsg, uint32_t nk,
-                          uint32_t* parts, uint32_t* zero, uint64_t zero_words, uint64_t& blocks, hipStream_t st,
+                          uint32_t* parts, uint32_t* ans, uint32_t* zero, uint64_t zero_words, hipStream_t st,
                           uint32_t sgm_keys = 0, uint32_t sgm_g = 1) {
-#if DPF_FOLD_GLDS_KERNEL
-    if constexpr (MT == 2 && NT == 2 && KG == 1) {
-        if (!sgm_keys) {
-            switch (fold_glds_mode()) {
-                case 1: return launch_glds<2, 2, 2, 1, 4>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
-                case 2: return launch_glds<2, 2, 2, 1, 3>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
-                case 3: return launch_glds<2, 2, 1, 1, 5>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
-                case 4: return launch_glds<2, 2, 1, 1, 6>(bits, wpk, dbs, nsg, nk, parts, zero, zero_words, blocks, st);
-                default: break;
-            }
-        }
-    }
-#endif
     constexpr int NW = 8 / NT * KG;
     // Resident workgroups only (one round): each takes a contiguous run of
     // whole staged blocks.  (A fixed 4 workgroups per CU left 1/4 - 3/4 of
@@ -1357,19 +1320,60 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
             n = 1;
         return n;
     }();
-    uint64_t spb;
-    split_chunks(nsg, (uint64_t)cu_count_fold() * (uint64_t)per_cu, SG, blocks, spb);
-    const uint32_t pe = fold_par_every();
-    if (sgm_keys && sgm_g == 4)
-        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 4>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, pe, sgm_keys);
-    else if (sgm_keys)
-        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 1>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, pe, sgm_keys);
-    else
-        hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, bits, wpk,
-                           reinterpret_cast<const uint4*>(dbs), nsg, nk, spb, parts, zero, zero_words, pe);
-    return hipGetLastError();
+    const uint64_t cap = g_fold_blocks.load(std::memory_order_relaxed);
+    const uint64_t msg = (uint64_t)fold_max_sg() / SG * SG > 0 ? (uint64_t)fold_max_sg() / SG * SG : SG;
+    const uint64_t resident = (uint64_t)cu_count_fold() * (uint64_t)per_cu;
+    // (The super-group-major layouts are measurement-only: one pass.)
+    const uint64_t per_pass = sgm_keys ? nsg : cap * msg;
+    for (uint64_t S0 = 0; S0 < nsg; S0 += per_pass) {
+        const uint64_t n = nsg - S0 < per_pass ? nsg - S0 : per_pass;
+        // enough workgroups that none folds more than msg super-groups
+        uint64_t want = (n + msg - 1) / msg;
+        if (want < resident) want = resident;
+        if (want > cap) want = cap;
+        const uint32_t* b = bits + (sgm_keys ? S0 / (sgm_g ? sgm_g : 1) * sgm_keys * (sgm_g ? sgm_g : 1) * 8 : S0 * 8);
+        const uint64_t wlim = wpk > S0 * 8 ? wpk - S0 * 8 : 0;
+        const uint8_t* d = dbs + S0 * 256 * 32;
+        uint32_t* z = S0 == 0 ? zero : nullptr;
+        const uint64_t zw = S0 == 0 ? zero_words : 0;
+        uint64_t blocks = 0;
+        hipError_t e = hipErrorUnknown;
+        bool done = false;
+#if DPF_FOLD_GLDS_KERNEL
+        if constexpr (MT == 2 && NT == 2 && KG == 1) {
+            if (!sgm_keys) {
+                done = true;
+                switch (fold_glds_mode()) {
+                    case 1: e = launch_glds<2, 2, 2, 1, 4>(b, wpk, wlim, d, n, nk, parts, z, zw, want, blocks, st); break;
+                    case 2: e = launch_glds<2, 2, 2, 1, 3>(b, wpk, wlim, d, n, nk, parts, z, zw, want, blocks, st); break;
+                    case 3: e = launch_glds<2, 2, 1, 1, 5>(b, wpk, wlim, d, n, nk, parts, z, zw, want, blocks, st); break;
+                    case 4: e = launch_glds<2, 2, 1, 1, 6>(b, wpk, wlim, d, n, nk, parts, z, zw, want, blocks, st); break;
+                    default: done = false;
+                }
+            }
+        }
+#endif
+        if (!done) {
+            uint64_t spb;
+            split_chunks(n, want, SG, blocks, spb);
+            if (sgm_keys && sgm_g == 4)
+                hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 4>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, b,
+                                   wpk, reinterpret_cast<const uint4*>(d), n, nk, spb, parts, z, zw, wlim, sgm_keys);
+            else if (sgm_keys)
+                hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 1>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, b,
+                                   wpk, reinterpret_cast<const uint4*>(d), n, nk, spb, parts, z, zw, wlim, sgm_keys);
+            else
+                hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, b, wpk,
+                                   reinterpret_cast<const uint4*>(d), n, nk, spb, parts, z, zw, wlim);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) return e;
+        const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
+        hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk,
+                           32u * MT * KG, 8u, ans, (uint64_t)8, 0u);
+        if (hipError_t e2 = hipGetLastError(); e2 != hipSuccess) return e2;
+    }
+    return hipSuccess;
 }
 }  // namespace
 
@@ -1409,33 +1413,27 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
         const uint32_t* b = bits + (sgm_keys ? (uint64_t)k0 * 8 * sgm_g : (uint64_t)k0 * words_per_key);
         uint32_t* zero = k0 == 0 ? ans : nullptr;
         const uint64_t zw = k0 == 0 ? (uint64_t)nkeys * 8 : 0;
-        uint64_t blocks = 0;
-        uint32_t mt;
+        uint32_t* a = ans + (uint64_t)k0 * 8;
         hipError_t e;
-        if (nk <= 32) e = launch_mfma_mt<1, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g), mt = 1;
+#define DPF_MT(MT_, NT_, SG_, KG_) \
+    launch_mfma_mt<MT_, NT_, SG_, KG_>(b, words_per_key, dbs, nsg, nk, parts, a, zero, zw, st, sgm_keys, sgm_g)
+        if (nk <= 32) e = DPF_MT(1, 2, 4, 1);
         else if (nk <= 64) {
-            mt = 2;
-            if (DPF_FOLD_SHAPE64 == 1) e = launch_mfma_mt<2, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-            else if (DPF_FOLD_SHAPE64 == 2) e = launch_mfma_mt<1, 2, 4, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-            else if (DPF_FOLD_SHAPE64 == 3) e = launch_mfma_mt<2, 4, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-            else e = launch_mfma_mt<2, 2, 2, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-        }
-        else if (nk <= 128) {
-            mt = 4;
-            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-            else e = launch_mfma_mt<4, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            if (DPF_FOLD_SHAPE64 == 1) e = DPF_MT(2, 2, 4, 1);
+            else if (DPF_FOLD_SHAPE64 == 2) e = DPF_MT(1, 2, 4, 2);
+            else if (DPF_FOLD_SHAPE64 == 3) e = DPF_MT(2, 4, 2, 1);
+            else e = DPF_MT(2, 2, 2, 1);
+        } else if (nk <= 128) {
+            if (DPF_FOLD_SHAPE == 1) e = DPF_MT(2, 4, 2, 2);
+            else e = DPF_MT(4, 2, 4, 1);
         } else {
-            mt = 8;
-            if (DPF_FOLD_SHAPE == 1) e = launch_mfma_mt<2, 4, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-            else if (DPF_FOLD_SHAPE == 2) e = launch_mfma_mt<4, 4, 2, 2>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-            else if (DPF_FOLD_SHAPE == 3) e = launch_mfma_mt<2, 8, 2, 4>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
-            else e = launch_mfma_mt<8, 2, 4, 1>(b, words_per_key, dbs, nsg, nk, parts, zero, zw, blocks, st, sgm_keys, sgm_g);
+            if (DPF_FOLD_SHAPE == 1) e = DPF_MT(2, 4, 2, 4);
+            else if (DPF_FOLD_SHAPE == 2) e = DPF_MT(4, 4, 2, 2);
+            else if (DPF_FOLD_SHAPE == 3) e = DPF_MT(2, 8, 2, 4);
+            else e = DPF_MT(8, 2, 4, 1);
         }
+#undef DPF_MT
         if (e != hipSuccess) return e;
-        const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
-        hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk, 32 * mt,
-                           8u, ans + (uint64_t)k0 * 8, (uint64_t)8, 0u);
-        if (hipError_t e2 = hipGetLastError(); e2 != hipSuccess) return e2;
     }
     return hipSuccess;
 }

@@ -42,10 +42,10 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
                                   uint32_t sgm_keys = 0, uint32_t sgm_g = 1);
 
 // Tuning / test limits of the fold launches: at most max_blocks workgroups
-// per launch (0 = the default, 1024), and the matrix-core fold reduces its
-// fp32 counts to parities every par_every super-groups (0 = the default and
-// maximum, 2^15 = 2^23 records; counts stay below fp32's exact 2^24).
-void set_fold_limits(uint32_t max_blocks, uint32_t par_every);
+// per launch (0 = the default, 1024), and at most max_sg super-groups per
+// matrix-core fold workgroup (0 = the default and maximum, 2^15 = 2^23
+// records, so its fp32 counts stay below 2^24); larger DBs fold in passes.
+void set_fold_limits(uint32_t max_blocks, uint32_t max_sg);
 
 // Fused PIR answer (k_pir_fused): the subtree EvalFull of keys [0, nkeys)
 // from their expanded records (launch_unpack) and the matrix-core fold over

@@ -506,11 +506,12 @@ def xor_fold_sliced_dev(d_bits, bits_stride: int, nkeys: int, d_dbs, nrec: int, 
                                          _ptr(d_work), _stream_handle(stream)))
 
 
-def set_fold_limits(max_blocks: int = 0, parity_every: int = 0) -> None:
+def set_fold_limits(max_blocks: int = 0, max_sg_per_block: int = 0) -> None:
     """Tuning / test limits of the fold launches (0 = default): workgroups per
-    launch, and super-groups between the matrix-core fold's parity reductions
-    (dpf_set_fold_limits).  Answers do not depend on them."""
-    _check(lib().dpf_set_fold_limits(max_blocks, parity_every))
+    launch, and super-groups (256 records) per matrix-core fold workgroup;
+    larger DBs fold in passes (dpf_set_fold_limits).  Answers do not depend
+    on them."""
+    _check(lib().dpf_set_fold_limits(max_blocks, max_sg_per_block))
 
 
 class PirDB:

@@ -257,12 +257,12 @@ func GetPirKernel() int {
 	return int(C.dpf_get_pir_kernel())
 }
 
-// SetFoldLimits caps the workgroups of a fold launch and sets how many
-// 256-record super-groups the matrix-core fold accumulates between parity
-// reductions (dpf_set_fold_limits; 0 = default).  Answers do not depend on
+// SetFoldLimits caps the workgroups of a fold launch and the 256-record
+// super-groups one matrix-core fold workgroup folds; larger DBs fold in
+// passes (dpf_set_fold_limits; 0 = default).  Answers do not depend on
 // either: tuning and tests only.
-func SetFoldLimits(maxBlocks uint32, parityEvery uint32) {
-	check(C.dpf_set_fold_limits(C.uint32_t(maxBlocks), C.uint32_t(parityEvery)))
+func SetFoldLimits(maxBlocks uint32, maxSgPerBlock uint32) {
+	check(C.dpf_set_fold_limits(C.uint32_t(maxBlocks), C.uint32_t(maxSgPerBlock)))
 }
 
 // PirKernelFor reports which kernel a PIR answer of this shape runs now

@@ -256,12 +256,13 @@ int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_strid
                             uint64_t nrec, uint8_t* d_ans, void* d_work, void* stream);
 /* Tuning / test limits of the XOR fold launches (process-wide; 0 = default):
  * at most max_blocks workgroups per fold launch (default and maximum 1024),
- * and the matrix-core fold reduces its fp32 counts to parities every
- * parity_every super-groups of 256 records (default and maximum 2^15, so a
- * count never exceeds 2^24, fp32's exact-integer bound, however many records
- * a workgroup folds).  Answers do not depend on either; tests use them to
- * force long per-workgroup runs and frequent reductions.  Returns 0. */
-int dpf_set_fold_limits(uint32_t max_blocks, uint32_t parity_every);
+ * and at most max_sg_per_block super-groups of 256 records per matrix-core
+ * fold workgroup (default and maximum 2^15).  The matrix-core fold's answer
+ * bits are parities of fp32 counts, exact up to 2^24; with at most 2^23
+ * records per workgroup no count gets there, and a DB with more super-groups
+ * than max_blocks x max_sg_per_block is folded in passes.  Answers do not
+ * depend on either; tests use them to force multi-pass folds.  Returns 0. */
+int dpf_set_fold_limits(uint32_t max_blocks, uint32_t max_sg_per_block);
 /* Kernel shape of dpf_pir_answer_sliced_dev (and of a sliced PIR handle):
  * DPF_PIR_SPLIT (default): a tree launch writes the selection bits to HBM
  * and a fold launch reads them back.  DPF_PIR_FUSED: where nkeys <= 64 and

@@ -201,15 +201,16 @@ def fold_limits():
 
 
 # the MFMA fold's answer bits are parities of fp32 counts, exact
-# only while a count stays <= 2^24.  The fold reduces its accumulators to
-# parities every `parity_every` super-groups, so a workgroup's run length no
-# longer matters.  Forced long runs (1-3 workgroups for the whole DB) and
-# reductions after every 1 / 3 / 5 super-groups must all give the answers of
+# only while a count stays <= 2^24.  No workgroup folds more than 2^15 super-
+# groups (2^23 records); a DB with more than 1024 x 2^15 super-groups folds in
+# passes.  Forced small limits (1-7 workgroups of 1-5 super-groups: many
+# passes, ragged last passes, several key groups) must all give the answers of
 # the default shape and of the LDS fold over the row-major DB.
-@pytest.mark.parametrize("max_blocks,par_every,nk,nrec", [
+@pytest.mark.parametrize("max_blocks,max_sg,nk,nrec", [
     (1, 1, 64, 8192), (3, 5, 33, 30000 - 7), (2, 3, 129, 20000), (1, 0, 256, 65536), (7, 2, 1, 9999),
+    (5, 4, 300, 12345),
 ])
-def test_sliced_fold_forced_long_runs_and_parity_reductions(fold_limits, max_blocks, par_every, nk, nrec):
+def test_sliced_fold_forced_passes(fold_limits, max_blocks, max_sg, nk, nrec):
     import torch
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(nk * 7 + nrec)
@@ -229,7 +230,7 @@ def test_sliced_fold_forced_long_runs_and_parity_reductions(fold_limits, max_blo
         return d_ans.cpu().numpy().reshape(nk, 32)
 
     base = run()
-    fold_limits(max_blocks, par_every)
+    fold_limits(max_blocks, max_sg)
     assert np.array_equal(run(), base)
     fold_limits(0, 0)
     assert np.array_equal(base, _fold(d_bits, stride, nk, payload, nrec, 32))
@@ -238,11 +239,11 @@ def test_sliced_fold_forced_long_runs_and_parity_reductions(fold_limits, max_blo
 
 
 def test_sliced_fold_counts_past_2p24_in_one_workgroup(fold_limits):
-    """One workgroup folds 2^24 + 2^21 records of an all-ones DB under
-    selection words that are mostly ones: every count passes 2^24 (fp32's
-    last exact integer, where a plain fp32 accumulation would round odd
-    partial sums), and the answer bit must be the parity of the number of
-    selected records."""
+    """2^24 + 2^21 records of an all-ones DB under selection words that are
+    mostly ones, with one workgroup per launch: a single run would count past
+    2^24 (fp32's last exact integer, where a plain fp32 accumulation rounds
+    odd partial sums); the launcher splits it into passes of 2^15 super-groups
+    and the answer bit must be the parity of the number of selected records."""
     import torch
     dev = torch.device("cuda", 0)
     nk, nrec = 32, (1 << 24) + (1 << 21)
