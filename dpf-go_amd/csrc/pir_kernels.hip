@@ -81,14 +81,15 @@ __device__ __forceinline__ void fold_prio(uint64_t done, uint64_t all) {
     (void)all;
 #endif
 }
-// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup
-// fence on all memory plus s_barrier, and its fence waits vmcnt(0): every
-// global load in flight -- the next block's operands, prefetched across the
-// barrier on purpose -- must land before any wave passes.  The folds only
-// need their LDS staging ordered, so this fences the local address space
-// (lgkmcnt) and leaves the prefetch in flight (r05, DPF_FOLD_RAW_BARRIER).
+// Workgroup barrier of the folds' LDS staging.  DPF_FOLD_RAW_BARRIER=1 fences
+// the local address space only (lgkmcnt) around s_barrier, so a global
+// prefetch issued before the barrier cannot be forced to land by it.  r05
+// measured it against __syncthreads(): identical (fold B=64 134.3 vs 134.3 us,
+// B=256 417 vs 416 us, PIR W=8 step 0.0765 vs 0.0765 ms;
+// profiles/r05/fold_barrier) -- the compiler already keeps the prefetch in
+// flight across __syncthreads -- so the default is the plain barrier.
 #ifndef DPF_FOLD_RAW_BARRIER
-#define DPF_FOLD_RAW_BARRIER 1
+#define DPF_FOLD_RAW_BARRIER 0
 #endif
 __device__ __forceinline__ void lds_barrier() {
 #if DPF_FOLD_RAW_BARRIER
