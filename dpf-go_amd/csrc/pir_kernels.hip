@@ -155,6 +155,21 @@ __device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool liv
 #ifndef DPF_FOLD_ABLATE
 #define DPF_FOLD_ABLATE 0   // measurement builds of k_fold_mfma: 1 = loads only, 2 = no HBM reads (wrong answers)
 #endif
+// Cache policy of k_fold_mfma's streamed operands (A/B builds): 0 = default,
+// 1 = DB pieces nontemporal, 2 = DB pieces and selection words nontemporal.
+#ifndef DPF_FOLD_NT
+#define DPF_FOLD_NT 0
+#endif
+typedef uint32_t fold_nt4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 fold_ld(const uint4* p) {
+    if constexpr (NT) {
+        const fold_nt4 v = __builtin_nontemporal_load(reinterpret_cast<const fold_nt4*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
 #ifndef DPF_FOLD_GLDS_DEFAULT
 #define DPF_FOLD_GLDS_DEFAULT 0   // launch_mfma_mt: LDS-DMA fold shape (fold_glds_mode)
 #endif
@@ -546,6 +561,61 @@ __global__ __launch_bounds__(256) void k_xor_parts(const uint32_t* __restrict__ 
     if (v) atomicXor(ans + (uint64_t)k * ans_words + off + i, v);
 }
 
+// Two-stage form (DPF_XOR_PARTS=2): a 256-thread block takes 64
+// consecutive answer words; its 4 waves XOR disjoint part subsets (8 loads in
+// flight per lane), LDS combines the 4, and one atomicXor per word per block
+// -- gridDim.y of them per word instead of 64.
+__global__ __launch_bounds__(256) void k_xor_parts2(const uint32_t* __restrict__ parts, uint64_t nparts, uint32_t nkeys,
+                                                    uint32_t pkeys, uint32_t pwords, uint32_t* __restrict__ ans,
+                                                    uint64_t ans_words, uint32_t off) {
+    __shared__ uint32_t s_x[3][64];
+    const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * 64 + l;
+    const bool live = t < nkeys * pwords;
+    const uint32_t k = live ? t / pwords : 0, i = live ? t % pwords : 0;
+    const uint64_t g = 4ull * gridDim.y;
+    uint64_t p = 4ull * blockIdx.y + wv;
+    uint32_t v = 0;
+    if (live) {
+        for (; p + 7 * g < nparts; p += 8 * g) {
+            uint32_t x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = parts[((p + u * g) * pkeys + k) * pwords + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v ^= x[u];
+        }
+        uint32_t x[7];
+#pragma unroll
+        for (int u = 0; u < 7; ++u) x[u] = p + u * g < nparts ? parts[((p + u * g) * pkeys + k) * pwords + i] : 0u;
+#pragma unroll
+        for (int u = 0; u < 7; ++u) v ^= x[u];
+    }
+    if (wv) s_x[wv - 1][l] = v;
+    __syncthreads();
+    if (wv == 0 && live) {
+        v ^= s_x[0][l] ^ s_x[1][l] ^ s_x[2][l];
+        if (v) atomicXor(ans + (uint64_t)k * ans_words + off + i, v);
+    }
+}
+
+#ifndef DPF_XOR_PARTS
+#define DPF_XOR_PARTS 1
+#endif
+// XOR nparts workgroup partials into the answers (stream-ordered after the fold).
+static hipError_t launch_xor_parts(const uint32_t* parts, uint64_t nparts, uint32_t nkeys, uint32_t pkeys,
+                                   uint32_t pwords, uint32_t* ans, uint64_t ans_words, uint32_t off, hipStream_t st) {
+    if (DPF_XOR_PARTS == 2) {
+        const uint64_t ys = (nparts + 31) / 32;
+        hipLaunchKernelGGL(k_xor_parts2, dim3((nkeys * pwords + 63) / 64, (uint32_t)(ys < 64 ? ys : 64)), dim3(256), 0,
+                           st, parts, nparts, nkeys, pkeys, pwords, ans, ans_words, off);
+    } else {
+        const uint32_t ys = (uint32_t)(nparts < 64 ? nparts : 64);
+        hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * pwords + 255) / 256, ys), dim3(256), 0, st, parts, nparts, nkeys,
+                           pkeys, pwords, ans, ans_words, off);
+    }
+    return hipGetLastError();
+}
+
 static int cu_count_fold() {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -670,11 +740,7 @@ hipError_t fold_pass(const FoldArgs& a, bool direct, int kw, uint32_t* ans, uint
         pkeys = 64;
     }
     if (e != hipSuccess) return e;
-    const uint32_t pwords = 8 * C;
-    const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
-    hipLaunchKernelGGL(k_xor_parts, dim3((a.nkeys * pwords + 255) / 256, ys), dim3(256), 0, st, a.parts, blocks,
-                       a.nkeys, pkeys, pwords, ans, ans_words, off);
-    return hipGetLastError();
+    return launch_xor_parts(a.parts, blocks, a.nkeys, pkeys, 8 * C, ans, ans_words, off, st);
 }
 
 }  // namespace
@@ -826,7 +892,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
             const uint32_t z = (uint32_t)at * 2654435761u;      // no HBM read (measurement build)
             const uint4 x = make_uint4(z, z ^ 0x5555u, z + 7u, ~z);
 #else
-            const uint4 x = *reinterpret_cast<const uint4*>(bits + (ok ? at : 0));
+            const uint4 x = fold_ld<(DPF_FOLD_NT >= 2)>(reinterpret_cast<const uint4*>(bits + (ok ? at : 0)));
 #endif
             v[i] = ok ? x : make_uint4(0, 0, 0, 0);
         }
@@ -851,7 +917,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
                 const uint32_t z = (uint32_t)((S * 256 + 32u * (w * NT + j) + r) * 2 + h) * 2246822519u;
                 B[sl][j] = make_uint4(z, z + 1u, z ^ 0xAAAAu, ~z);           // no HBM read (measurement build)
 #else
-                B[sl][j] = dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h];
+                B[sl][j] = fold_ld<(DPF_FOLD_NT >= 1)>(&dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h]);
 #endif
             }
         }
@@ -1369,10 +1435,8 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
             e = hipGetLastError();
         }
         if (e != hipSuccess) return e;
-        const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
-        hipLaunchKernelGGL(k_xor_parts, dim3((nk * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nk,
-                           32u * MT * KG, 8u, ans, (uint64_t)8, 0u);
-        if (hipError_t e2 = hipGetLastError(); e2 != hipSuccess) return e2;
+        if (hipError_t e2 = launch_xor_parts(parts, blocks, nk, 32u * MT * KG, 8u, ans, 8, 0u, st); e2 != hipSuccess)
+            return e2;
     }
     return hipSuccess;
 }
@@ -1404,10 +1468,7 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
         hipLaunchKernelGGL(k_fold_sliced_direct<1>, dim3((uint32_t)blocks), dim3(256), 0, st, bits, words_per_key,
                            reinterpret_cast<const uint4*>(dbs), nsg, nkeys, spb, parts, ans, (uint64_t)nkeys * 8);
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-        const uint32_t ys = (uint32_t)(blocks < 64 ? blocks : 64);
-        hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * 8 + 255) / 256, ys), dim3(256), 0, st, parts, blocks, nkeys, kb, 8u,
-                           ans, (uint64_t)8, 0u);
-        return hipGetLastError();
+        return launch_xor_parts(parts, blocks, nkeys, kb, 8u, ans, 8, 0u, st);
     }
     for (uint32_t k0 = 0; k0 < nkeys; k0 += 256) {
         const uint32_t nk = nkeys - k0 < 256 ? nkeys - k0 : 256;
@@ -1811,10 +1872,7 @@ hipError_t launch_pir_fused(const uint32_t* ek, uint32_t nkeys, uint32_t stop, u
         hipLaunchKernelGGL(k_pir_fused<true>, dim3(blocks), dim3(kFzThreads), 0, st, ek, nkeys, stop, prefix_bits,
                            prefix, reinterpret_cast<const uint4*>(dbs), nsg, parts, ans, (uint64_t)nkeys * 8);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-    const uint32_t ys = blocks < 64 ? blocks : 64;
-    hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * 8 + 255) / 256, ys), dim3(256), 0, st, parts, (uint64_t)blocks, nkeys,
-                       64u, 8u, ans, (uint64_t)8, 0u);
-    return hipGetLastError();
+    return launch_xor_parts(parts, blocks, nkeys, 64u, 8u, ans, 8, 0u, st);
 }
 
 #else
