@@ -587,6 +587,9 @@ __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekey
 #ifndef DPF_EVAL_EARLY
 #define DPF_EVAL_EARLY 1
 #endif
+#ifndef DPF_EVAL_PERSIST
+#define DPF_EVAL_PERSIST 0   // k_eval_persist for frontier Eval with wave-uniform keys (env DPF_EVAL_PERSIST)
+#endif
 #ifndef DPF_EVAL_PREFETCH
 #define DPF_EVAL_PREFETCH 0   // strided k_eval2: next pair's inputs requested before the current walk (A/B)
 #endif
@@ -645,6 +648,111 @@ __global__ __launch_bounds__(kBlock, 4) void k_eval2(const uint32_t* __restrict_
                             eval_pair_in<UNI>(ekeys, stop, logN, xs, nq, pts_per_key, fseed, ft, L, q0));
     }
 #endif
+}
+
+// Persistent batched Eval (r05): one 1024-thread workgroup per CU fills its
+// T-table once and strides over the query pairs; the next pair's points and
+// frontier nodes move into per-wave LDS slots by LDS-DMA
+// (global_load_lds_dwordx4 / _dword) while the current pair walks, so they
+// cost no VGPRs (k_eval2 sits at the 128-VGPR limit; a register prefetch of
+// the next pair spilled and ran slower, DPF_EVAL_PREFETCH above) and no
+// workgroup waits out a fresh table fill or its first gathers.
+// Pipeline per thread, iteration i: read x(i) and node(i) from LDS; read
+// x(i+1), issue node(i+1)'s gathers; issue x(i+2); walk pair i.  The slots are
+// this wave's own, so no barrier: the compiler waits vmcnt(0) before the first
+// slot read of an iteration (the DMAs issued one walk earlier), and T-table
+// reads (a different LDS object) never wait on them.
+// UNI only: a wave's 64 pairs are 128 consecutive queries of one key, and nq
+// is even (pts_per_key % 128 == 0), so a pair's points are one 16-byte load.
+constexpr int kEvalPBlock = 1024;
+struct EvalSlots {
+    uint4 x[2][64];      // x(i), x(i+1): {x0, x1} as two uint64
+    uint4 n0[64], n1[64]; // frontier seeds of pair i's two queries
+    uint32_t t0[64], t1[64];   // aligned dwords holding their t bytes
+};
+__device__ __forceinline__ void eval_lgkm0() {              // s_waitcnt lgkmcnt(0), nothing else
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));
+#endif
+}
+__device__ __forceinline__ void glds(const void* g, void* l, int size) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (size == 16)
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+    else
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 4, 0, 0);
+#else
+    (void)g;
+    (void)l;
+    (void)size;
+#endif
+}
+__global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t* __restrict__ ekeys, uint32_t stop,
+                                                                 uint32_t logN, const uint64_t* __restrict__ xs,
+                                                                 uint64_t nq, uint64_t pts_per_key,
+                                                                 const uint4* __restrict__ fseed,
+                                                                 const uint8_t* __restrict__ ft, uint32_t L,
+                                                                 uint8_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+    __shared__ __attribute__((aligned(16))) EvalSlots s_sl[kEvalPBlock / 64];
+    const uint32_t lane = threadIdx.x & 63;
+    EvalSlots& sl = s_sl[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    const uint64_t npairs = nq / 2;
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // every wave runs the same number of iterations (tail pairs clamped, not stored)
+    const uint64_t iters = (npairs + nthr - 1) / nthr;
+    auto pair_of = [&](uint64_t i) __attribute__((always_inline)) {
+        const uint64_t p = i * nthr + gt;
+        return p < npairs ? p : npairs - 1;
+    };
+    auto issue_x = [&](uint64_t i, int slot) __attribute__((always_inline)) {
+        glds(xs + 2 * pair_of(i), &sl.x[slot][0], 16);
+    };
+    auto issue_nodes = [&](uint64_t i, int slot) __attribute__((always_inline)) {
+        const uint4 xv = sl.x[slot][lane];
+        const uint64_t x0 = ((uint64_t)xv.y << 32) | xv.x, x1 = ((uint64_t)xv.w << 32) | xv.z;
+        const uint64_t key = pair_key<true>(2 * pair_of(i), pts_per_key);
+        const uint64_t m = (1ull << L) - 1;
+        const uint64_t i0 = (key << L) + ((x0 >> (logN - L)) & m), i1 = (key << L) + ((x1 >> (logN - L)) & m);
+        eval_lgkm0();                                    // this wave's reads of the node slots are done
+        glds(fseed + i0, &sl.n0[0], 16);
+        glds(fseed + i1, &sl.n1[0], 16);
+        glds(ft + (i0 & ~3ull), &sl.t0[0], 4);
+        glds(ft + (i1 & ~3ull), &sl.t1[0], 4);
+    };
+    if (iters > 0) {
+        issue_x(0, 0);
+        if (iters > 1) issue_x(1, 1);
+    }
+    fill_table(s_tab);
+    __builtin_amdgcn_s_setprio(3);
+    if (iters > 0) issue_nodes(0, 0);
+    for (uint64_t it = 0; it < iters; ++it) {
+        if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
+        else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
+        else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
+        const int cur = (int)(it & 1);
+        PairIn p;
+        const uint4 xv = sl.x[cur][lane];
+        p.x0 = ((uint64_t)xv.y << 32) | xv.x;
+        p.x1 = ((uint64_t)xv.w << 32) | xv.z;
+        {
+            const uint4 a = sl.n0[lane], b = sl.n1[lane];
+            const uint64_t key = pair_key<true>(2 * pair_of(it), pts_per_key);
+            const uint64_t m = (1ull << L) - 1;
+            const uint32_t i0 = (uint32_t)((key << L) + ((p.x0 >> (logN - L)) & m)) & 3u;
+            const uint32_t i1 = (uint32_t)((key << L) + ((p.x1 >> (logN - L)) & m)) & 3u;
+            p.n0.s = {a.x, a.y, a.z, a.w};
+            p.n1.s = {b.x, b.y, b.z, b.w};
+            p.n0.t = (sl.t0[lane] >> (8 * i0)) & 0xffu;
+            p.n1.t = (sl.t1[lane] >> (8 * i1)) & 0xffu;
+        }
+        if (it + 1 < iters) issue_nodes(it + 1, cur ^ 1);
+        if (it + 2 < iters) issue_x(it + 2, cur);
+        const uint64_t pr = it * nthr + gt;
+        if (pr < npairs) eval_pair_walk<true>(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, 2 * pr, p);
+    }
 }
 
 #ifndef DPF_EVAL_TRIE_KERNEL
@@ -1150,6 +1258,18 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
         return hipGetLastError();
     }
 #endif
+    // Persistent form (k_eval_persist): needs the frontier and wave-uniform keys.
+    static const int persist = [] {
+        const char* e = getenv("DPF_EVAL_PERSIST");
+        return e && *e ? atoi(e) : DPF_EVAL_PERSIST;
+    }();
+    if (persist && L > 0 && pts_per_key % 128 == 0 && nq == nkeys * pts_per_key && nq >= 2 * (uint64_t)kEvalPBlock) {
+        const uint64_t want = (nq / 2 + kEvalPBlock - 1) / kEvalPBlock;
+        const uint64_t cus = (uint64_t)cu_count();
+        hipLaunchKernelGGL(k_eval_persist, dim3((uint32_t)(want < cus ? want : cus)), dim3(kEvalPBlock), 0, st, ek, stop,
+                           logN, xs, nq, pts_per_key, fseed, ft, L, out);
+        return hipGetLastError();
+    }
 #if DPF_EVAL_PAIRS
     const uint64_t nthreads = (nq + 1) / 2;
     const uint32_t block = pick_block(nthreads, kBlock);

@@ -155,11 +155,8 @@ __device__ __forceinline__ uint2 valid_mask(uint64_t cc, uint64_t nrec, bool liv
 #ifndef DPF_FOLD_ABLATE
 #define DPF_FOLD_ABLATE 0   // measurement builds of k_fold_mfma: 1 = loads only, 2 = no HBM reads (wrong answers)
 #endif
-// Cache policy of k_fold_mfma's streamed operands (A/B builds): 0 = default,
-// 1 = DB pieces nontemporal, 2 = DB pieces and selection words nontemporal.
-#ifndef DPF_FOLD_NT
-#define DPF_FOLD_NT 0
-#endif
+// A streamed 16-byte operand; NT: a nontemporal load (the `nt` cache policy),
+// for DB slices too large to stay in the caches between batches (launch_mfma_mt).
 typedef uint32_t fold_nt4 __attribute__((ext_vector_type(4)));
 template <bool NT>
 __device__ __forceinline__ uint4 fold_ld(const uint4* p) {
@@ -561,58 +558,12 @@ __global__ __launch_bounds__(256) void k_xor_parts(const uint32_t* __restrict__ 
     if (v) atomicXor(ans + (uint64_t)k * ans_words + off + i, v);
 }
 
-// Two-stage form (DPF_XOR_PARTS=2): a 256-thread block takes 64
-// consecutive answer words; its 4 waves XOR disjoint part subsets (8 loads in
-// flight per lane), LDS combines the 4, and one atomicXor per word per block
-// -- gridDim.y of them per word instead of 64.
-__global__ __launch_bounds__(256) void k_xor_parts2(const uint32_t* __restrict__ parts, uint64_t nparts, uint32_t nkeys,
-                                                    uint32_t pkeys, uint32_t pwords, uint32_t* __restrict__ ans,
-                                                    uint64_t ans_words, uint32_t off) {
-    __shared__ uint32_t s_x[3][64];
-    const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t t = blockIdx.x * 64 + l;
-    const bool live = t < nkeys * pwords;
-    const uint32_t k = live ? t / pwords : 0, i = live ? t % pwords : 0;
-    const uint64_t g = 4ull * gridDim.y;
-    uint64_t p = 4ull * blockIdx.y + wv;
-    uint32_t v = 0;
-    if (live) {
-        for (; p + 7 * g < nparts; p += 8 * g) {
-            uint32_t x[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) x[u] = parts[((p + u * g) * pkeys + k) * pwords + i];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v ^= x[u];
-        }
-        uint32_t x[7];
-#pragma unroll
-        for (int u = 0; u < 7; ++u) x[u] = p + u * g < nparts ? parts[((p + u * g) * pkeys + k) * pwords + i] : 0u;
-#pragma unroll
-        for (int u = 0; u < 7; ++u) v ^= x[u];
-    }
-    if (wv) s_x[wv - 1][l] = v;
-    __syncthreads();
-    if (wv == 0 && live) {
-        v ^= s_x[0][l] ^ s_x[1][l] ^ s_x[2][l];
-        if (v) atomicXor(ans + (uint64_t)k * ans_words + off + i, v);
-    }
-}
-
-#ifndef DPF_XOR_PARTS
-#define DPF_XOR_PARTS 1
-#endif
 // XOR nparts workgroup partials into the answers (stream-ordered after the fold).
 static hipError_t launch_xor_parts(const uint32_t* parts, uint64_t nparts, uint32_t nkeys, uint32_t pkeys,
                                    uint32_t pwords, uint32_t* ans, uint64_t ans_words, uint32_t off, hipStream_t st) {
-    if (DPF_XOR_PARTS == 2) {
-        const uint64_t ys = (nparts + 31) / 32;
-        hipLaunchKernelGGL(k_xor_parts2, dim3((nkeys * pwords + 63) / 64, (uint32_t)(ys < 64 ? ys : 64)), dim3(256), 0,
-                           st, parts, nparts, nkeys, pkeys, pwords, ans, ans_words, off);
-    } else {
-        const uint32_t ys = (uint32_t)(nparts < 64 ? nparts : 64);
-        hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * pwords + 255) / 256, ys), dim3(256), 0, st, parts, nparts, nkeys,
-                           pkeys, pwords, ans, ans_words, off);
-    }
+    const uint32_t ys = (uint32_t)(nparts < 64 ? nparts : 64);
+    hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * pwords + 255) / 256, ys), dim3(256), 0, st, parts, nparts, nkeys,
+                       pkeys, pwords, ans, ans_words, off);
     return hipGetLastError();
 }
 
@@ -845,7 +796,7 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 // the kernel moved the large-tile accumulators out of AGPRs and spilled them:
 // 2.5x slower at 256 keys, r05.)  wlim: selection words per key row from
 // `bits` (the row stride stays wpk), so a pass can start mid-row.
-template <int MT, int NT, int SG, int KG, int SGM = 0>
+template <int MT, int NT, int SG, int KG, int SGM = 0, bool NTDB = false>
 __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
@@ -892,7 +843,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
             const uint32_t z = (uint32_t)at * 2654435761u;      // no HBM read (measurement build)
             const uint4 x = make_uint4(z, z ^ 0x5555u, z + 7u, ~z);
 #else
-            const uint4 x = fold_ld<(DPF_FOLD_NT >= 2)>(reinterpret_cast<const uint4*>(bits + (ok ? at : 0)));
+            const uint4 x = *reinterpret_cast<const uint4*>(bits + (ok ? at : 0));
 #endif
             v[i] = ok ? x : make_uint4(0, 0, 0, 0);
         }
@@ -917,7 +868,7 @@ __global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_
                 const uint32_t z = (uint32_t)((S * 256 + 32u * (w * NT + j) + r) * 2 + h) * 2246822519u;
                 B[sl][j] = make_uint4(z, z + 1u, z ^ 0xAAAAu, ~z);           // no HBM read (measurement build)
 #else
-                B[sl][j] = fold_ld<(DPF_FOLD_NT >= 1)>(&dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h]);
+                B[sl][j] = fold_ld<NTDB>(&dbs[(S * 256 + 32u * (w * NT + j) + r) * 2 + h]);
 #endif
             }
         }
@@ -1369,6 +1320,20 @@ static int fold_glds_mode() {
 
 #endif
 
+// The DB pieces of a fold over at least this many DB bytes are loaded
+// nontemporal.  r05 (tools/r05_xp.sh, profiles/r05/fold_nt/): at 2^24 x 32 B
+// (512 MiB, twice the chip's last-level cache) the fold took 123-127 us
+// instead of 134-135; at an N = 8 rank's 64 MiB slice, which stays cached
+// between batches, 25-26 instead of 24.4.  DPF_FOLD_NT_MIN (bytes) overrides.
+constexpr uint64_t kFoldNtMinBytes = 256ull << 20;
+static uint64_t fold_nt_min_bytes() {
+    static const uint64_t v = [] {
+        const char* e = getenv("DPF_FOLD_NT_MIN");
+        return e && *e ? strtoull(e, nullptr, 0) : kFoldNtMinBytes;
+    }();
+    return v;
+}
+
 // One key group (<= 32 * MT * KG keys) over the sliced DB: passes of at most
 // (workgroup cap) x kFoldMaxSgPerBlock super-groups, each a fold launch whose
 // workgroups fold <= kFoldMaxSgPerBlock super-groups (fp32-exact counts, see
@@ -1392,6 +1357,7 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
     const uint64_t resident = (uint64_t)cu_count_fold() * (uint64_t)per_cu;
     // (The super-group-major layouts are measurement-only: one pass.)
     const uint64_t per_pass = sgm_keys ? nsg : cap * msg;
+    const bool ntdb = nsg * 256 * 32 >= fold_nt_min_bytes();
     for (uint64_t S0 = 0; S0 < nsg; S0 += per_pass) {
         const uint64_t n = nsg - S0 < per_pass ? nsg - S0 : per_pass;
         // enough workgroups that none folds more than msg super-groups
@@ -1429,6 +1395,9 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
             else if (sgm_keys)
                 hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 1>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, b,
                                    wpk, reinterpret_cast<const uint4*>(d), n, nk, spb, parts, z, zw, wlim, sgm_keys);
+            else if (ntdb)
+                hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 0, true>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st,
+                                   b, wpk, reinterpret_cast<const uint4*>(d), n, nk, spb, parts, z, zw, wlim);
             else
                 hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, b, wpk,
                                    reinterpret_cast<const uint4*>(d), n, nk, spb, parts, z, zw, wlim);
