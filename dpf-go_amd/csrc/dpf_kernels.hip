@@ -557,13 +557,12 @@ __device__ __forceinline__ PairIn eval_pair_in(const uint32_t* __restrict__ ekey
     p.n1 = eval_start(ekeys + key1 * rec, key1, p.x1, logN, fseed, ft, L);
     return p;
 }
+// The pair's two answer bits (bit 0: query q0, bit 8: q0 + 1).
 template <bool UNI>
-__device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
-                                               uint64_t nq, uint64_t pts_per_key, const uint4* __restrict__ fseed,
-                                               uint32_t L, uint8_t* __restrict__ out, const uint32_t* s_tab,
-                                               uint64_t q0, PairIn p) {
-    const bool two = q0 + 1 < nq;
-    const uint64_t q1 = two ? q0 + 1 : q0;
+__device__ __forceinline__ uint32_t eval_pair_bits(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
+                                                   uint64_t nq, uint64_t pts_per_key, const uint4* __restrict__ fseed,
+                                                   uint32_t L, const uint32_t* s_tab, uint64_t q0, PairIn p) {
+    const uint64_t q1 = q0 + 1 < nq ? q0 + 1 : q0;
     const uint64_t key0 = pair_key<UNI>(q0, pts_per_key), key1 = UNI ? key0 : q1 / pts_per_key;
     const uint64_t rec = (uint64_t)(stop + 2) * 8;
     const uint32_t* ek0 = ekeys + key0 * rec;
@@ -580,8 +579,16 @@ __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekey
     const Blk f0 = load_blk(ek0 + 8 + 8 * stop);
     o0 = leaf_fix(o0, p.n0.t, f0);
     o1 = leaf_fix(o1, p.n1.t, UNI ? f0 : load_blk(ek1 + 8 + 8 * stop));
-    out[q0] = eval_bit(o0, p.x0);
-    if (two) out[q1] = eval_bit(o1, p.x1);
+    return (uint32_t)eval_bit(o0, p.x0) | ((uint32_t)eval_bit(o1, p.x1) << 8);
+}
+template <bool UNI>
+__device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
+                                               uint64_t nq, uint64_t pts_per_key, const uint4* __restrict__ fseed,
+                                               uint32_t L, uint8_t* __restrict__ out, const uint32_t* s_tab,
+                                               uint64_t q0, PairIn p) {
+    const uint32_t b = eval_pair_bits<UNI>(ekeys, stop, logN, nq, pts_per_key, fseed, L, s_tab, q0, p);
+    out[q0] = (uint8_t)b;
+    if (q0 + 1 < nq) out[q0 + 1] = (uint8_t)(b >> 8);
 }
 
 #ifndef DPF_EVAL_EARLY
@@ -721,37 +728,51 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
         glds(ft + (i0 & ~3ull), &sl.t0[0], 4);
         glds(ft + (i1 & ~3ull), &sl.t1[0], 4);
     };
-    if (iters > 0) {
-        issue_x(0, 0);
-        if (iters > 1) issue_x(1, 1);
-    }
+    // Pair i's points and nodes into registers (the compiler waits vmcnt(0)
+    // first: the slot DMAs, issued one walk earlier, and the previous pair's
+    // output stores, issued after the previous wait -- so a walk's stores
+    // are never waited on right after they issue).
+    auto read_pair = [&](uint64_t i) __attribute__((always_inline)) {
+        PairIn p;
+        const uint4 xv = sl.x[i & 1][lane];
+        p.x0 = ((uint64_t)xv.y << 32) | xv.x;
+        p.x1 = ((uint64_t)xv.w << 32) | xv.z;
+        const uint4 a = sl.n0[lane], b = sl.n1[lane];
+        const uint64_t key = pair_key<true>(2 * pair_of(i), pts_per_key);
+        const uint64_t m = (1ull << L) - 1;
+        const uint32_t i0 = (uint32_t)((key << L) + ((p.x0 >> (logN - L)) & m)) & 3u;
+        const uint32_t i1 = (uint32_t)((key << L) + ((p.x1 >> (logN - L)) & m)) & 3u;
+        p.n0.s = {a.x, a.y, a.z, a.w};
+        p.n1.s = {b.x, b.y, b.z, b.w};
+        p.n0.t = (sl.t0[lane] >> (8 * i0)) & 0xffu;
+        p.n1.t = (sl.t1[lane] >> (8 * i1)) & 0xffu;
+        return p;
+    };
+    if (iters == 0) return;                               // uniform over the grid
+    issue_x(0, 0);
+    if (iters > 1) issue_x(1, 1);
     fill_table(s_tab);
     __builtin_amdgcn_s_setprio(3);
-    if (iters > 0) issue_nodes(0, 0);
+    issue_nodes(0, 0);
+    PairIn p = read_pair(0);
+    if (iters > 1) issue_nodes(1, 1);
+    if (iters > 2) issue_x(2, 0);
     for (uint64_t it = 0; it < iters; ++it) {
         if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
         else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
-        const int cur = (int)(it & 1);
-        PairIn p;
-        const uint4 xv = sl.x[cur][lane];
-        p.x0 = ((uint64_t)xv.y << 32) | xv.x;
-        p.x1 = ((uint64_t)xv.w << 32) | xv.z;
-        {
-            const uint4 a = sl.n0[lane], b = sl.n1[lane];
-            const uint64_t key = pair_key<true>(2 * pair_of(it), pts_per_key);
-            const uint64_t m = (1ull << L) - 1;
-            const uint32_t i0 = (uint32_t)((key << L) + ((p.x0 >> (logN - L)) & m)) & 3u;
-            const uint32_t i1 = (uint32_t)((key << L) + ((p.x1 >> (logN - L)) & m)) & 3u;
-            p.n0.s = {a.x, a.y, a.z, a.w};
-            p.n1.s = {b.x, b.y, b.z, b.w};
-            p.n0.t = (sl.t0[lane] >> (8 * i0)) & 0xffu;
-            p.n1.t = (sl.t1[lane] >> (8 * i1)) & 0xffu;
-        }
-        if (it + 1 < iters) issue_nodes(it + 1, cur ^ 1);
-        if (it + 2 < iters) issue_x(it + 2, cur);
         const uint64_t pr = it * nthr + gt;
-        if (pr < npairs) eval_pair_walk<true>(ekeys, stop, logN, nq, pts_per_key, fseed, L, out, s_tab, 2 * pr, p);
+        const uint32_t b = eval_pair_bits<true>(ekeys, stop, logN, nq, pts_per_key, fseed, L, s_tab, 2 * pr, p);
+        // unconditional (the last iteration rereads its own slots): a
+        // conditional read leaves the DMAs possibly pending at the join, and
+        // the compiler then waits on this pair's stores before issue_nodes
+        p = read_pair(it + 1 < iters ? it + 1 : it);
+        if (pr < npairs) {
+            out[2 * pr] = (uint8_t)b;
+            out[2 * pr + 1] = (uint8_t)(b >> 8);
+        }
+        if (it + 2 < iters) issue_nodes(it + 2, (int)(it & 1));
+        if (it + 3 < iters) issue_x(it + 3, (int)((it + 1) & 1));
     }
 }
 

@@ -1231,7 +1231,9 @@ __global__ __launch_bounds__(256) void k_slice_db(const uint4* __restrict__ db, 
 // configs[4] against the MFMA fold's 103): with 4 or 16 keys its per-key
 // scalar loads serialise (131 / 388 us against 104 / 107,
 // profiles/r04/fold_ab/).
-template <int KB>
+// (Nontemporal DB loads, as the matrix-core fold takes them above 256 MiB,
+// measured 95.2-95.8 against 93.9-94.4 us here at 2^24 records: not used.)
+template <int KB, bool NTDB = false>
 __global__ __launch_bounds__(256) void k_fold_sliced_direct(const uint32_t* __restrict__ bits, uint64_t wpk,
                                                             const uint4* __restrict__ dbs, uint64_t nsg,
                                                             uint32_t nkeys, uint64_t sg_per_block,
@@ -1268,12 +1270,13 @@ __global__ __launch_bounds__(256) void k_fold_sliced_direct(const uint32_t* __re
     };
     uint64_t S = s0;
     for (; S + 1 < s1; S += 2) {
-        const uint4 a0 = dbs[(S * 256 + n) * 2], b0 = dbs[(S * 256 + n) * 2 + 1];
-        const uint4 a1 = dbs[((S + 1) * 256 + n) * 2], b1 = dbs[((S + 1) * 256 + n) * 2 + 1];
+        const uint4 a0 = fold_ld<NTDB>(&dbs[(S * 256 + n) * 2]), b0 = fold_ld<NTDB>(&dbs[(S * 256 + n) * 2 + 1]);
+        const uint4 a1 = fold_ld<NTDB>(&dbs[((S + 1) * 256 + n) * 2]);
+        const uint4 b1 = fold_ld<NTDB>(&dbs[((S + 1) * 256 + n) * 2 + 1]);
         fold(S, a0, b0);
         fold(S + 1, a1, b1);
     }
-    if (S < s1) fold(S, dbs[(S * 256 + n) * 2], dbs[(S * 256 + n) * 2 + 1]);
+    if (S < s1) fold(S, fold_ld<NTDB>(&dbs[(S * 256 + n) * 2]), fold_ld<NTDB>(&dbs[(S * 256 + n) * 2 + 1]));
     // parts[block][key][8]: wave w holds answer words 2w (lanes 0-31) and 2w+1.
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
@@ -1320,11 +1323,12 @@ static int fold_glds_mode() {
 
 #endif
 
-// The DB pieces of a fold over at least this many DB bytes are loaded
-// nontemporal.  r05 (tools/r05_xp.sh, profiles/r05/fold_nt/): at 2^24 x 32 B
-// (512 MiB, twice the chip's last-level cache) the fold took 123-127 us
-// instead of 134-135; at an N = 8 rank's 64 MiB slice, which stays cached
-// between batches, 25-26 instead of 24.4.  DPF_FOLD_NT_MIN (bytes) overrides.
+// The DB pieces of a matrix-core fold over at least this many DB bytes are
+// loaded nontemporal.  r05 (tools/r05_nt.sh, profiles/r05/fold_nt/, B = 64,
+// fold us, nontemporal vs default): 2^24 x 32 B (512 MiB, twice the chip's
+// last-level cache) 123-125 vs 135-138, and B = 16 95 vs 105-107; 2^23 66-69
+// vs 67-74; but 2^22 39-40 vs 35-36 and 2^21 (an N = 8 rank) 25.5 vs 24.7:
+// slices that stay cached between batches lose.  DPF_FOLD_NT_MIN overrides.
 constexpr uint64_t kFoldNtMinBytes = 256ull << 20;
 static uint64_t fold_nt_min_bytes() {
     static const uint64_t v = [] {

@@ -2,7 +2,8 @@
 (HBM/MFMA-bound) of batch i?  configs[4] shape (64 keys, logN=24, one GPU):
 one stream (tree, fold, tree, fold ...) against two streams with the
 selection bits double-buffered (fold(i) waits for tree(i); tree(i+2) waits
-for fold(i)).  Prints ms per batch for each.
+for fold(i)).  Prints ms per batch for each.  PB=b: an N = 2^b rank's share
+(subtree 0 of depth b and its 2^(logN-b)-record DB slice).
   python tools/pir_overlap.py [batches]"""
 import os, sys, json, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,8 +18,9 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 dpf.gpu_init_devices([0])
 logN, nk = 24, int(os.environ.get("NK", "64"))
-nrec = 1 << logN
-kl, per_key = dpf.key_len(logN), dpf.evalfull_len(logN)
+pb = int(os.environ.get("PB", "0"))
+nrec = 1 << (logN - pb)
+kl, per_key = dpf.key_len(logN), dpf.evalfull_len(logN) >> pb
 s0_ = torch.cuda.current_stream(dev)
 db = torch.from_numpy(synth.db_bytes(nrec * 32)).to(dev)
 dbs = torch.empty(dpf.pir_db_sliced_size(nrec), dtype=torch.uint8, device=dev)
@@ -39,7 +41,7 @@ sB = torch.cuda.Stream(dev, priority=-1) if prio else torch.cuda.Stream(dev)
 
 
 def tree(i, st):
-    dpf.evalfull_subtree_dev(keys, kl, nk, logN, 0, 0, bits[i % 2], work[i % 2], device=0, stream=st)
+    dpf.evalfull_subtree_dev(keys, kl, nk, logN, pb, 0, bits[i % 2], work[i % 2], device=0, stream=st)
 
 
 def fold(i, st):
@@ -85,5 +87,5 @@ for r in range(3):
 seq(2); torch.cuda.synchronize(); a0 = [x.clone() for x in ans]
 pipe(2); torch.cuda.synchronize()
 out["same_answers"] = all(torch.equal(a, b) for a, b in zip(a0, ans))
-out["nk"], out["fold_priority"] = nk, prio
+out["nk"], out["fold_priority"], out["prefix_bits"] = nk, prio, pb
 print(json.dumps(out))

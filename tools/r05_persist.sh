@@ -26,3 +26,19 @@ import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
     print(r["Name"].split("(")[0][:50], r["Calls"], round(float(r["AverageNs"]) / 1e3, 2), "us")
 PY
+# PIR tree of batch i+1 beside the fold of batch i on a second stream, at the
+# N = 8 / 4 rank shapes (prefix 3 / 2) and on one GPU.
+for pb in 3 2 0; do
+  PB=$pb timeout -k 10 120 python3 tools/pir_overlap.py 300 > "$OUT/overlap_pb$pb.log" 2>&1 || { echo "overlap pb=$pb failed"; tail -5 "$OUT/overlap_pb$pb.log"; exit 1; }
+  echo "pb=$pb $(tail -1 "$OUT/overlap_pb$pb.log")" | tee -a "$OUT/ab.txt"
+done
+# The fold's ablations again with nontemporal DB loads (the product at 2^24).
+export FOLD_MODE=mfma
+for r in 1 2 3; do
+  for b in fold_bench bin/fold_bench_ablate1 bin/fold_bench_ablate2; do
+    timeout -k 10 60 tools/$b 64 32 24 > "$OUT/ab.json" 2>&1
+    rc=$?   # the ablation builds compute wrong answers on purpose (exit 1, "ok": false)
+    if [ $rc -ne 0 ] && ! grep -q '"fold_us"' "$OUT/ab.json"; then echo "$b failed rc=$rc"; cat "$OUT/ab.json"; exit 1; fi
+    python3 -c "import json; d=json.load(open('$OUT/ab.json')); print('$r $(basename $b) 64 32 24', d['fold_us'], 'us', d['GBs'], 'GB/s')" | tee -a "$OUT/ablate_nt.txt"
+  done
+done
