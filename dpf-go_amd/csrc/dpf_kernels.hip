@@ -677,9 +677,20 @@ struct EvalSlots {
     uint4 n0[64], n1[64]; // frontier seeds of pair i's two queries
     uint32_t t0[64], t1[64];   // aligned dwords holding their t bytes
 };
-__device__ __forceinline__ void eval_lgkm0() {              // s_waitcnt lgkmcnt(0), nothing else
+// s_waitcnt vmcnt(0) as a compiler memory barrier: the slot DMAs have
+// landed and no slot read is hoisted above the wait (hipcc's own waits did
+// not cover every slot read once the loop was rotated).
+__device__ __forceinline__ void eval_vm0() {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+}
+// s_waitcnt lgkmcnt(0) that is also a compiler memory barrier: this wave's
+// LDS reads of a slot stay above it (and complete before it ends), and the
+// LDS-DMA that overwrites the slot stays below it.
+__device__ __forceinline__ void eval_lgkm0() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
 }
 __device__ __forceinline__ void glds(const void* g, void* l, int size) {
@@ -700,7 +711,11 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
                                                                  const uint4* __restrict__ fseed,
                                                                  const uint8_t* __restrict__ ft, uint32_t L,
                                                                  uint8_t* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+    // The table must sit at LDS address 0, where every lookup's address is
+    // its byte index (the ds_read offset field is 16 bits): the stricter
+    // alignment places it first.  Behind the 72 KiB of slots it cost one
+    // v_add_u32 per lookup, 320 per walk level.
+    __shared__ __attribute__((aligned(256))) uint32_t s_tab[kTabWords];
     __shared__ __attribute__((aligned(16))) EvalSlots s_sl[kEvalPBlock / 64];
     const uint32_t lane = threadIdx.x & 63;
     EvalSlots& sl = s_sl[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
@@ -728,11 +743,12 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
         glds(ft + (i0 & ~3ull), &sl.t0[0], 4);
         glds(ft + (i1 & ~3ull), &sl.t1[0], 4);
     };
-    // Pair i's points and nodes into registers (the compiler waits vmcnt(0)
-    // first: the slot DMAs, issued one walk earlier, and the previous pair's
-    // output stores, issued after the previous wait -- so a walk's stores
-    // are never waited on right after they issue).
+    // Pair i's points and nodes into registers, after vmcnt(0): the slot
+    // DMAs, issued one walk earlier, and the previous pair's output stores,
+    // issued after the previous wait -- so a walk's stores are never waited
+    // on right after they issue.
     auto read_pair = [&](uint64_t i) __attribute__((always_inline)) {
+        eval_vm0();
         PairIn p;
         const uint4 xv = sl.x[i & 1][lane];
         p.x0 = ((uint64_t)xv.y << 32) | xv.x;
@@ -756,13 +772,16 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
     issue_nodes(0, 0);
     PairIn p = read_pair(0);
     if (iters > 1) issue_nodes(1, 1);
-    if (iters > 2) issue_x(2, 0);
+    if (iters > 2) {
+        eval_lgkm0();
+        issue_x(2, 0);
+    }
     for (uint64_t it = 0; it < iters; ++it) {
         if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
         else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
         const uint64_t pr = it * nthr + gt;
-        const uint32_t b = eval_pair_bits<true>(ekeys, stop, logN, nq, pts_per_key, fseed, L, s_tab, 2 * pr, p);
+        const uint32_t b = eval_pair_bits<true>(ekeys, stop, logN, nq, pts_per_key, fseed, L, s_tab, 2 * pair_of(it), p);
         // unconditional (the last iteration rereads its own slots): a
         // conditional read leaves the DMAs possibly pending at the join, and
         // the compiler then waits on this pair's stores before issue_nodes
@@ -772,7 +791,10 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
             out[2 * pr + 1] = (uint8_t)(b >> 8);
         }
         if (it + 2 < iters) issue_nodes(it + 2, (int)(it & 1));
-        if (it + 3 < iters) issue_x(it + 3, (int)((it + 1) & 1));
+        if (it + 3 < iters) {
+            eval_lgkm0();
+            issue_x(it + 3, (int)((it + 1) & 1));
+        }
     }
 }
 
