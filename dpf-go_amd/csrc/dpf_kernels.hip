@@ -595,7 +595,7 @@ __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekey
 #define DPF_EVAL_EARLY 1
 #endif
 #ifndef DPF_EVAL_PERSIST
-#define DPF_EVAL_PERSIST 0   // k_eval_persist for frontier Eval with wave-uniform keys (env DPF_EVAL_PERSIST)
+#define DPF_EVAL_PERSIST 1   // k_eval_persist for frontier Eval with wave-uniform keys (env DPF_EVAL_PERSIST=0: k_eval2)
 #endif
 #ifndef DPF_EVAL_PREFETCH
 #define DPF_EVAL_PREFETCH 0   // strided k_eval2: next pair's inputs requested before the current walk (A/B)
