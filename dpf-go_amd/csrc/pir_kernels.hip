@@ -1354,14 +1354,23 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_mfma<MT, NT, SG, KG>, 64 * NW, 0) != hipSuccess || n < 1)
             n = 1;
+        const char* e = getenv("DPF_FOLD_PER_CU");            // A/B runs: at most this many per CU
+        if (e && atoi(e) > 0 && atoi(e) < n) n = atoi(e);
         return n;
     }();
     const uint64_t cap = g_fold_blocks.load(std::memory_order_relaxed);
     const uint64_t msg = (uint64_t)fold_max_sg() / SG * SG > 0 ? (uint64_t)fold_max_sg() / SG * SG : SG;
-    const uint64_t resident = (uint64_t)cu_count_fold() * (uint64_t)per_cu;
     // (The super-group-major layouts are measurement-only: one pass.)
     const uint64_t per_pass = sgm_keys ? nsg : cap * msg;
     const bool ntdb = nsg * 256 * 32 >= fold_nt_min_bytes();
+    // Two workgroups per CU instead of the occupancy limit (3 at 33-64 keys)
+    // for cached DB slices and for the one-key-tile shape: fewer partials to
+    // combine and less per-workgroup overhead (r05, tools/r05_fpercu.sh,
+    // profiles/r05/fold_blocks/, medians of 5: 2^21 x 32 B 22.6 vs 24.7 us,
+    // 2^22 34.8 vs 36.0, B = 16 at 2^24 91.9 vs 96.6, B = 32 96.3 vs 99.8;
+    // but B = 64 at 2^23 / 2^24 67.9 / 130.7 vs 67.0 / 125.9).
+    const uint64_t pcu = (!ntdb || MT == 1) && per_cu > 2 ? 2 : (uint64_t)per_cu;
+    const uint64_t resident = (uint64_t)cu_count_fold() * pcu;
     for (uint64_t S0 = 0; S0 < nsg; S0 += per_pass) {
         const uint64_t n = nsg - S0 < per_pass ? nsg - S0 : per_pass;
         // enough workgroups that none folds more than msg super-groups

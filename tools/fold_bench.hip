@@ -43,6 +43,8 @@ int main(int argc, char** argv) {
     // records), built once here as the PIR server does at load time; its
     // answers must equal the Four-Russians / direct fold's for every key.
     const bool mfma = getenv("FOLD_MODE") && getenv("FOLD_MODE")[0] == 'm';
+    // FOLD_BLOCKS=n: at most n workgroups per fold launch (dpf_set_fold_limits).
+    if (getenv("FOLD_BLOCKS")) dpfk::set_fold_limits((uint32_t)atoi(getenv("FOLD_BLOCKS")), 0);
     void* dbs = nullptr;
     float slice_ms = 0;
     std::vector<uint8_t> ref((size_t)nkeys * rec_bytes);

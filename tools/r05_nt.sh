@@ -8,7 +8,7 @@ cd "$REPO"
 OUT="gpurun_out/${1:-r05_nt}"; mkdir -p "$OUT"
 export FOLD_MODE=mfma
 for r in 1 2 3; do
-  for cfg in "64 32 21" "64 32 22" "64 32 23" "64 32 24" "16 32 24" "256 32 24"; do
+  for cfg in "64 32 21" "64 32 22" "64 32 23" "64 32 24" "1 32 24" "16 32 24" "256 32 24"; do
     for nt in 0 4611686018427387904; do
       DPF_FOLD_NT_MIN=$nt timeout -k 10 60 tools/fold_bench $cfg > "$OUT/fb.json" 2>&1 || { echo "fold_bench $cfg failed"; cat "$OUT/fb.json"; exit 1; }
       python3 -c "import json; d=json.load(open('$OUT/fb.json')); print('$r $cfg nt=' + ('always' if '$nt' == '0' else 'never'), d['fold_us'], 'us', d['GBs'], 'GB/s ok', d['ok'])" | tee -a "$OUT/nt.txt"
