@@ -901,9 +901,14 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
 def wl_pir(c: Ctx) -> dict:
     a, dpf = c.args, c.dpf
     from dpf import synth
-    logN, nk = a.pir_logN, a.batch
+    logN = a.pir_logN
     nrec = 1 << logN
     W = c.world if c.world > 1 else max(1, a.emulate_world)
+    # --pir-per-gpu: B queries per server GPU, every GPU folding all B x W of
+    # them over its DB slice (weak scaling: per-GPU AES and fold work stay
+    # those of one GPU's B-query batch); otherwise B queries in total (strong).
+    weak = bool(getattr(a, "pir_per_gpu", False))
+    nk = a.batch * W if weak else a.batch
     d_db, lo, hi = pir_setup(c, W)
     ka, result, t_wall, k_ms = pir_time(c, W, d_db, lo, hi, nk, a.steps, a.warmup)
     if a.check and c.rank == 0 and W == c.world:
@@ -917,9 +922,10 @@ def wl_pir(c: Ctx) -> dict:
     pb = (W - 1).bit_length()
     aes = nk * (3 * (1 << (stop_of(logN) - pb)) - 2)
     line = c.line(metric="2-server PIR answered queries/sec per server (EvalFull logN=24 + XOR fold)",
-                  value=nk / sec, unit="queries/s", ms_per_step=sec * 1e3, scaling="strong",
+                  value=nk / sec, unit="queries/s", ms_per_step=sec * 1e3, scaling="weak" if weak else "strong",
                   data="synthetic DB (SplitMix64) + keys",
                   config={"workload": f"PIR, DB 2^{logN} x 32 B sharded over {W} GPU(s), batch {nk}"
+                                      + (f" ({a.batch} per GPU)" if weak else "")
                                       + f" ({'bitsliced' if dpf.get_aes_impl() else 'lds-ttable'} AES)"
                                       + (" (rank 0's share timed on 1 GPU)" if W != c.world else "")
                                       + " (BASELINE configs[4])", "logN": logN, "batch": nk,
@@ -979,8 +985,14 @@ def sub_workloads(c: Ctx) -> dict:
     a.steps, a.warmup = min(a.steps, 20), min(a.warmup, 5)
     a.no_api, a.no_sweep, a.emulate_world = True, True, 1
     out = {}
+    # At N > 1 the PIR server is also timed in its weak form (--batch queries
+    # per GPU): at N = 1 it is the same run as "pir".
+    runs = [("eval", wl_eval, False), ("split", wl_split, False), ("pir", wl_pir, False)]
+    if c.world > 1:
+        runs.append(("pir_weak", wl_pir, True))
     try:
-        for name, fn in (("eval", wl_eval), ("split", wl_split), ("pir", wl_pir)):
+        for name, fn, per_gpu in runs:
+            a.pir_per_gpu = per_gpu
             ln = fn(c)
             keep = {k: ln[k] for k in ("metric", "value", "unit", "ms_per_step", "scaling", "aes_blocks_per_s")}
             keep["steps"] = a.steps
@@ -1036,7 +1048,8 @@ def dry_run(args) -> None:
         same_shape = wl in ("evalfull", "eval") or world == 1
         line = {"dry_run": True, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "max_rank_s": float(t.item()), "local_ranks": os.environ.get("LOCAL_WORLD_SIZE"),
-                "workload": wl, "scaling": "strong" if wl in ("split", "pir") else "weak"}
+                "workload": wl,
+                "scaling": "strong" if wl == "split" or (wl == "pir" and not args.pir_per_gpu) else "weak"}
         line["roofline"] = prg_roofline(1e11, "k_evalfull<7, true, false>", 1.0, 512 << 20, workload=wl,
                                         profiled_shape=same_shape)
         finalize(line, args, world, folded=False)
@@ -1060,6 +1073,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--pir-fold", choices=["mfma", "lds"], default="mfma",
                     help="pir: XOR fold on the matrix cores over the bit-sliced DB (default) or the LDS fold")
+    ap.add_argument("--pir-per-gpu", action="store_true",
+                    help="pir: --batch queries per GPU (total batch B x N, weak scaling) instead of B in total")
     ap.add_argument("--emulate-world", type=int, default=1,
                     help="split/pir on 1 GPU: time rank 0's share of a W-way split")
     ap.add_argument("--event-every", type=int, default=10,

@@ -268,7 +268,8 @@ __device__ __forceinline__ uint32_t mmo_quad(const uint8_t* tab, uint32_t lo, co
     return s ^ x;
 }
 
-__device__ __forceinline__ void fill_table(uint32_t* tab) {
+// Without the closing barrier: the caller adds its own LDS writes first.
+__device__ __forceinline__ void fill_table_nobar(uint32_t* tab) {
     // Row e: 32 copies of Te0[e], then 32 copies of rotl8(Te0[e]); 16-byte stores.
     for (uint32_t i = threadIdx.x; i < 256 * 16; i += blockDim.x) {
         uint32_t e = i >> 4, q = i & 15;
@@ -276,6 +277,9 @@ __device__ __forceinline__ void fill_table(uint32_t* tab) {
         if (q >= 8) v = rotl(v, 8);
         reinterpret_cast<uint4*>(tab)[e * 16 + q] = make_uint4(v, v, v, v);
     }
+}
+__device__ __forceinline__ void fill_table(uint32_t* tab) {
+    fill_table_nobar(tab);
     __syncthreads();
 }
 

@@ -55,6 +55,12 @@
 #ifndef DPF_WALK_BATCH
 #define DPF_WALK_BATCH 1   // tree kernels' root-to-subtree walks: batched single-block rounds
 #endif
+#ifndef DPF_WALK_CW_LDS
+#define DPF_WALK_CW_LDS 1  // walks of a one-key workgroup read their correction words from LDS (staged once)
+#endif
+#ifndef DPF_DFS_CW_LDS
+#define DPF_DFS_CW_LDS 0   // ... and so does the subtree expansion below them (A/B)
+#endif
 
 namespace dpfk {
 
@@ -72,7 +78,22 @@ struct Ctx {
     uint4* nseed;       // node mode: seed cursor
     uint8_t* nt;        // node mode: t cursor
     uint32_t groups;    // 4-leaf groups finished (wave priority steps, prio_step)
+    const uint32_t* cwl;   // the key's CWs staged in LDS (8 words per level), or nullptr
 };
+
+// Level lvl's correction word for the expansion: from the LDS copy when the
+// workgroup staged one (DPF_DFS_CW_LDS), else from the key.
+template <bool RAW>
+__device__ __forceinline__ CW ctx_cw(const Ctx& c, uint32_t lvl) {
+#if DPF_DFS_CW_LDS
+    if (c.cwl != nullptr) {
+        const uint4 a = *reinterpret_cast<const uint4*>(c.cwl + 8 * lvl);
+        const uint2 b = *reinterpret_cast<const uint2*>(c.cwl + 8 * lvl + 4);
+        return CW{{a.x, a.y, a.z, a.w}, b.x, b.y};
+    }
+#endif
+    return key_cw<RAW>(c.ks, lvl);
+}
 
 // Issue priority by progress.  A SIMD's waves issue oldest-first, so of the
 // 4 waves sharing one, the oldest finishes its subtree first and the
@@ -140,10 +161,10 @@ __device__ __forceinline__ Blk bsel(bool b, const Blk& x, const Blk& y) {
 // loop body was ~85 KiB of code (22 AES-MMO bodies).
 template <bool B, bool RAW>
 __device__ __forceinline__ void leaves4(const Ctx& c, uint32_t lvl, const Node& n, uint8_t* p) {
-    CW cw = key_cw<RAW>(c.ks, lvl);
+    CW cw = ctx_cw<RAW>(c, lvl);
     Node L, R;
     expand<B>(c.tab, c.lo, n, cw, L, R);
-    CW cw1 = key_cw<RAW>(c.ks, lvl + 1);
+    CW cw1 = ctx_cw<RAW>(c, lvl + 1);
     Blk o0 = {}, o1 = {}, o2, o3;
     // Only the pending child stays live through the first iteration (a
     // select of L or R at the top of each iteration kept both live: 5 more
@@ -191,7 +212,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         // apart left ~4 MiB of half-written lines per XCD (its whole L2) and
         // made WRITE_SIZE 1.26x the output.  Leaves are unchanged, only which
         // lane computes them.
-        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - 3);
+        CW cw = ctx_cw<RAW>(c, lvl0 + DMAX - 3);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
         const bool odd = (threadIdx.x & 1u) != 0;
@@ -224,10 +245,10 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         // Bottom two levels of a frontier at once: 4 seeds = 64 contiguous
         // bytes and their 4 t bytes as one 32-bit store (one byte store per
         // node made the NODES pass write 2.2x its 17 B per node).
-        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - 2);
+        CW cw = ctx_cw<RAW>(c, lvl0 + DMAX - 2);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
-        CW cw1 = key_cw<RAW>(c.ks, lvl0 + DMAX - 1);
+        CW cw1 = ctx_cw<RAW>(c, lvl0 + DMAX - 1);
         Node q[4];
         expand<B>(c.tab, c.lo, L, cw1, q[0], q[1]);
         expand<B>(c.tab, c.lo, R, cw1, q[2], q[3]);
@@ -239,7 +260,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
         c.nt += 4;
         prio_step<DMAX>(c);
     } else if constexpr (D == 1) {
-        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - 1);
+        CW cw = ctx_cw<RAW>(c, lvl0 + DMAX - 1);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
         if constexpr (NODES) {
@@ -253,7 +274,7 @@ __device__ __forceinline__ void dfs(Ctx& c, uint32_t lvl0, const Node& n) {
             c.outp += 32;
         }
     } else {
-        CW cw = key_cw<RAW>(c.ks, lvl0 + DMAX - D);
+        CW cw = ctx_cw<RAW>(c, lvl0 + DMAX - D);
         Node L, R;
         expand<B>(c.tab, c.lo, n, cw, L, R);
         // The right child is the only node live across the left subtree.
@@ -310,9 +331,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     const uint64_t t_start = wall_clock64();
 #endif
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-    fill_table(s_tab);
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kTreeBlock
-    if (u >= nunits) return;
     uint64_t key = u >> units_log;
     if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
     const uint64_t local = u & ((1ull << units_log) - 1);
@@ -323,7 +342,40 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     } else {
         c.ks = {ekeys + key * ((uint64_t)(stop + 2) * 8), nullptr, 0, 0};
     }
+    // Correction words of the walk levels 0..ltop-1 staged in LDS when the
+    // whole workgroup evaluates one key (r05).  Read in the walk by scalar
+    // loads, each level's CW put an s_waitcnt lgkmcnt(0) -- the counter the
+    // T-table lookups also use -- into the middle of the level's dependent
+    // AES rounds, exposing an L2 (or HBM) round trip per level of a walk
+    // that runs while the CU is otherwise idle.  Here lane l of wave 0 loads
+    // level l's CW with vector loads issued before the table fill, and the
+    // walks read it from LDS (in-order returns: no wait beyond the round's own).
+    __shared__ __attribute__((aligned(16))) uint32_t s_cw[8 * 64];
+    const uint32_t Bw = blockDim.x;
+    const bool cw_lds = DPF_WALK_CW_LDS && UNIFORM && (Bw & (Bw - 1)) == 0 && stop <= 64 &&
+                        units_log >= 31u - (uint32_t)__builtin_clz(Bw) &&
+                        (uint64_t)blockIdx.x * Bw < nunits;   // workgroup-uniform
+    const bool cw_mine = cw_lds && threadIdx.x < (DPF_DFS_CW_LDS ? stop : ltop);
+    CW cw_pre{};
+    if (cw_mine) cw_pre = key_cw<RAW>(c.ks, threadIdx.x);   // per-lane level: vector loads
+    fill_table_nobar(s_tab);
+    if (cw_mine) {
+        *reinterpret_cast<uint4*>(s_cw + 8 * threadIdx.x) = make_uint4(cw_pre.s.c0, cw_pre.s.c1, cw_pre.s.c2, cw_pre.s.c3);
+        *reinterpret_cast<uint2*>(s_cw + 8 * threadIdx.x + 4) = make_uint2(cw_pre.tl, cw_pre.tr);
+    }
+    __syncthreads();
+    if (u >= nunits) return;
+    auto lds_cw = [&](uint32_t lvl) __attribute__((always_inline)) {
+        const uint4 a = *reinterpret_cast<const uint4*>(s_cw + 8 * lvl);
+        const uint2 b = *reinterpret_cast<const uint2*>(s_cw + 8 * lvl + 4);
+        return CW{{a.x, a.y, a.z, a.w}, b.x, b.y};
+    };
+    // The shared walk below runs only in one-key workgroups, where cw_lds holds.
+    auto shared_cw = [&](uint32_t lvl) __attribute__((always_inline)) {
+        return DPF_WALK_CW_LDS ? lds_cw(lvl) : key_cw<RAW>(c.ks, lvl);
+    };
     c.groups = 0;
+    c.cwl = DPF_DFS_CW_LDS && cw_lds ? s_cw : nullptr;
 #if DPF_PRIO_STEPS
     __builtin_amdgcn_s_setprio(3);
 #endif
@@ -365,7 +417,8 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
         __shared__ uint32_t s_front[5 * kFs];   // SoA: word k of node j at k * kFs + j
         const uint32_t B = blockDim.x;
         const uint32_t W = 31u - (uint32_t)__builtin_clz(B);
-        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W && B <= (uint32_t)kTreeBlock) {   // uniform
+        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W && B <= (uint32_t)kTreeBlock &&
+            (cw_lds || !DPF_WALK_CW_LDS)) {   // uniform
             // Paths of the shared walk: 2^F, F = 6, or DPF_QUAD_FAN with the
             // quad form when the workgroup has the 4 * 2^F lanes for it.
             const uint32_t F = DPF_QUAD_WALK && DPF_QUAD_FAN > 6 && W >= DPF_QUAD_FAN + 2 ? DPF_QUAD_FAN : 6;
@@ -390,7 +443,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
                     uint32_t col = j == 0 ? n.s.c0 : j == 1 ? n.s.c1 : j == 2 ? n.s.c2 : n.s.c3;
                     uint32_t t = n.t;
                     for (uint32_t i = 0; i < l1; ++i) {
-                        const CW cw = key_cw<RAW>(c.ks, i);
+                        const CW cw = shared_cw(i);
                         const uint32_t cwj = j == 0 ? cw.s.c0 : j == 1 ? cw.s.c1 : j == 2 ? cw.s.c2 : cw.s.c3;
                         walk_step_quad(c.tab, c.lo, qk, j, col, t, cwj, cw.tl, cw.tr,
                                        (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
@@ -402,7 +455,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
                 const uint64_t subj = (sub - threadIdx.x) + ((uint64_t)threadIdx.x << (W - 6));
                 Node m = n;
                 for (uint32_t i = 0; i < l1; ++i) {
-                    CW cw = key_cw<RAW>(c.ks, i);
+                    CW cw = shared_cw(i);
                     walk_step<DPF_WALK_BATCH>(c.tab, c.lo, m, cw, (uint32_t)(subj >> (ltop - 1 - i)) & 1u);
                 }
                 put(threadIdx.x, m);
@@ -431,9 +484,12 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
 #endif
         }
     }
-    for (uint32_t i = lvl; i < ltop; ++i) {
-        CW cw = key_cw<RAW>(c.ks, i);
-        walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, cw, (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
+    if (cw_lds) {
+        for (uint32_t i = lvl; i < ltop; ++i)
+            walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, lds_cw(i), (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
+    } else {
+        for (uint32_t i = lvl; i < ltop; ++i)
+            walk_step<DPF_WALK_BATCH>(c.tab, c.lo, n, key_cw<RAW>(c.ks, i), (uint32_t)(sub >> (ltop - 1 - i)) & 1u);
     }
 #ifdef DPF_WAVE_TIMES
     const uint64_t t_walk = wall_clock64();
@@ -561,7 +617,8 @@ __device__ __forceinline__ PairIn eval_pair_in(const uint32_t* __restrict__ ekey
 template <bool UNI>
 __device__ __forceinline__ uint32_t eval_pair_bits(const uint32_t* __restrict__ ekeys, uint32_t stop, uint32_t logN,
                                                    uint64_t nq, uint64_t pts_per_key, const uint4* __restrict__ fseed,
-                                                   uint32_t L, const uint32_t* s_tab, uint64_t q0, PairIn p) {
+                                                   uint32_t L, const uint32_t* s_tab, uint64_t q0, PairIn p,
+                                                   const uint32_t* cwp = nullptr) {
     const uint64_t q1 = q0 + 1 < nq ? q0 + 1 : q0;
     const uint64_t key0 = pair_key<UNI>(q0, pts_per_key), key1 = UNI ? key0 : q1 / pts_per_key;
     const uint64_t rec = (uint64_t)(stop + 2) * 8;
@@ -569,14 +626,28 @@ __device__ __forceinline__ uint32_t eval_pair_bits(const uint32_t* __restrict__ 
     const uint32_t* ek1 = ekeys + key1 * rec;
     const uint8_t* tab = reinterpret_cast<const uint8_t*>(s_tab);
     const uint32_t lo = (threadIdx.x & 31u) * 4u;
-    for (uint32_t i = fseed != nullptr ? L : 0; i < stop; ++i) {
-        const CW cw0 = load_cw(ek0, i), cw1 = UNI ? cw0 : load_cw(ek1, i);
-        walk_step2<DPF_EVAL_BATCH>(tab, lo, p.n0, cw0, path_bit(p.x0, logN - 1 - i), p.n1, cw1,
-                                   path_bit(p.x1, logN - 1 - i));
+    const uint32_t i0 = fseed != nullptr ? L : 0;
+    if (UNI && cwp != nullptr) {
+        // The key's records from level i0 on, staged in LDS by the caller
+        // (k_eval_persist): no scalar load -- whose lgkmcnt(0) would stall
+        // the level's first AES round -- inside the walk.
+        for (uint32_t i = i0; i < stop; ++i) {
+            const uint4 a = *reinterpret_cast<const uint4*>(cwp + 8 * (i - i0));
+            const uint2 b = *reinterpret_cast<const uint2*>(cwp + 8 * (i - i0) + 4);
+            const CW cw{{a.x, a.y, a.z, a.w}, b.x, b.y};
+            walk_step2<DPF_EVAL_BATCH>(tab, lo, p.n0, cw, path_bit(p.x0, logN - 1 - i), p.n1, cw,
+                                       path_bit(p.x1, logN - 1 - i));
+        }
+    } else {
+        for (uint32_t i = i0; i < stop; ++i) {
+            const CW cw0 = load_cw(ek0, i), cw1 = UNI ? cw0 : load_cw(ek1, i);
+            walk_step2<DPF_EVAL_BATCH>(tab, lo, p.n0, cw0, path_bit(p.x0, logN - 1 - i), p.n1, cw1,
+                                       path_bit(p.x1, logN - 1 - i));
+        }
     }
     Blk o0, o1;
     mmo2<DPF_EVAL_BATCH>(tab, lo, KeyFixed<false>{}, p.n0.s, o0, KeyFixed<false>{}, p.n1.s, o1);
-    const Blk f0 = load_blk(ek0 + 8 + 8 * stop);
+    const Blk f0 = UNI && cwp != nullptr ? load_blk(cwp + 8 * (stop - i0)) : load_blk(ek0 + 8 + 8 * stop);
     o0 = leaf_fix(o0, p.n0.t, f0);
     o1 = leaf_fix(o1, p.n1.t, UNI ? f0 : load_blk(ek1 + 8 + 8 * stop));
     return (uint32_t)eval_bit(o0, p.x0) | ((uint32_t)eval_bit(o1, p.x1) << 8);
@@ -596,6 +667,9 @@ __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekey
 #endif
 #ifndef DPF_EVAL_PERSIST
 #define DPF_EVAL_PERSIST 1   // k_eval_persist for frontier Eval with wave-uniform keys (env DPF_EVAL_PERSIST=0: k_eval2)
+#endif
+#ifndef DPF_EVAL_CW_LDS
+#define DPF_EVAL_CW_LDS 1   // k_eval_persist: each pair's key records staged in LDS by LDS-DMA (A/B: 0)
 #endif
 #ifndef DPF_EVAL_PREFETCH
 #define DPF_EVAL_PREFETCH 0   // strided k_eval2: next pair's inputs requested before the current walk (A/B)
@@ -676,6 +750,9 @@ struct EvalSlots {
     uint4 x[2][64];      // x(i), x(i+1): {x0, x1} as two uint64
     uint4 n0[64], n1[64]; // frontier seeds of pair i's two queries
     uint32_t t0[64], t1[64];   // aligned dwords holding their t bytes
+#if DPF_EVAL_CW_LDS
+    uint32_t cw[2][64];  // pair i's key records, levels L..stop-1 and the final CW (parity of i)
+#endif
 };
 // s_waitcnt vmcnt(0) as a compiler memory barrier: the slot DMAs have
 // landed and no slot read is hoisted above the wait (hipcc's own waits did
@@ -728,6 +805,11 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
         const uint64_t p = i * nthr + gt;
         return p < npairs ? p : npairs - 1;
     };
+    const uint64_t rec = (uint64_t)(stop + 2) * 8;
+    const uint32_t ncw = (stop - L) * 8 + 4;
+    const bool cw_slots = DPF_EVAL_CW_LDS && ncw <= 64;      // uniform
+    (void)rec;
+    (void)cw_slots;
     auto issue_x = [&](uint64_t i, int slot) __attribute__((always_inline)) {
         glds(xs + 2 * pair_of(i), &sl.x[slot][0], 16);
     };
@@ -742,6 +824,12 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
         glds(fseed + i1, &sl.n1[0], 16);
         glds(ft + (i0 & ~3ull), &sl.t0[0], 4);
         glds(ft + (i1 & ~3ull), &sl.t1[0], 4);
+#if DPF_EVAL_CW_LDS
+        // The key's records from level L: 8 words per level, then the final
+        // CW (dpf.go:186-188, :206), one word per lane.  Slot parity i & 1:
+        // walk i - 2 (the slot's last reader) is done, by the wait above.
+        if (cw_slots && lane < ncw) glds(ekeys + key * rec + 8 + 8 * L + lane, &sl.cw[slot][0], 4);
+#endif
     };
     // Pair i's points and nodes into registers, after vmcnt(0): the slot
     // DMAs, issued one walk earlier, and the previous pair's output stores,
@@ -781,7 +869,13 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
         else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
         const uint64_t pr = it * nthr + gt;
-        const uint32_t b = eval_pair_bits<true>(ekeys, stop, logN, nq, pts_per_key, fseed, L, s_tab, 2 * pair_of(it), p);
+#if DPF_EVAL_CW_LDS
+        const uint32_t* cwp = cw_slots ? &sl.cw[it & 1][0] : nullptr;
+#else
+        const uint32_t* cwp = nullptr;
+#endif
+        const uint32_t b = eval_pair_bits<true>(ekeys, stop, logN, nq, pts_per_key, fseed, L, s_tab, 2 * pair_of(it), p,
+                                                cwp);
         // unconditional (the last iteration rereads its own slots): a
         // conditional read leaves the DMAs possibly pending at the join, and
         // the compiler then waits on this pair's stores before issue_nodes
