@@ -1318,6 +1318,12 @@ uint32_t eval_frontier_level(uint32_t stop, uint64_t pts_per_key) {
     // node (L = 9 at 1024 points per key), used when L >= 4.
     uint32_t L = 0;
     while (L < kMaxFrontierHbm && L < stop && (2ull << (L + 1)) <= pts_per_key) ++L;
+    // DPF_EVAL_LEVEL_SHIFT=n (measurement only): the frontier n levels deeper.
+    static const int shift = [] {
+        const char* e = getenv("DPF_EVAL_LEVEL_SHIFT");
+        return e && *e ? atoi(e) : 0;
+    }();
+    if (L >= 4 && shift > 0 && L + (uint32_t)shift < stop && L + (uint32_t)shift <= kMaxFrontierHbm) L += shift;
     return L >= 4 ? L : 0;
 }
 
