@@ -117,6 +117,10 @@ def test_bench_gpus_flag_spawns_ranks():
     assert p["roofline"]["traffic"] is None and "traffic_note" in p["roofline"]
     # ... and every workload line carries its own CPU baseline (queries/s here).
     assert p["cpu_baseline"]["unit"] == "queries/s" and p["cpu_baseline"]["value"] > 0
+    # PIR with a fixed batch is strong scaling; --batch queries per GPU is weak.
+    assert p["scaling"] == "strong"
+    w = run("--workload", "pir", "--pir-per-gpu", "--no-cpu-baseline")
+    assert w["scaling"] == "weak"
 
 
 def test_xor_rows_matches_numpy():
