@@ -221,11 +221,15 @@ def test_logN32_single_key_property():
 
 
 @pytest.mark.parametrize("logN,nk,ppk", [(13, 8, 256), (14, 5, 1000), (20, 6, 1024), (20, 3, 3000), (32, 4, 512),
-                                         (63, 2, 700), (15, 3, 257), (20, 600, 1024), (17, 2100, 128)])
+                                         (63, 2, 700), (15, 3, 257), (20, 600, 1024), (17, 2100, 128),
+                                         (20, 8, 256), (21, 8, 256)])
 def test_eval_frontier_path_vs_oracle(logN, nk, ppk):
     """Shared-frontier Eval kernel (taken when a key has >= 256 points).
     (20, 600, 1024) gives the persistent kernel two ragged passes over its
-    resident threads; (17, 2100, 128) one partial pass."""
+    resident threads; (17, 2100, 128) one partial pass.  The persistent
+    kernel stages a pair's key records in LDS when they fit 64 words:
+    (20, 8, 256) is the largest such walk (7 levels + final CW = 60 words),
+    (21, 8, 256) and (32, 4, 512) take the scalar-load walk."""
     _, ka, _ = _keys(nk, logN, first=8000 + logN + ppk)
     xs = synth.eval_points(nk, ppk, logN)
     xs[:, 0] = 0
