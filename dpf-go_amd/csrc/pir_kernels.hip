@@ -1354,9 +1354,11 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fold_mfma<MT, NT, SG, KG>, 64 * NW, 0) != hipSuccess || n < 1)
             n = 1;
-        const char* e = getenv("DPF_FOLD_PER_CU");            // A/B runs: at most this many per CU
-        if (e && atoi(e) > 0 && atoi(e) < n) n = atoi(e);
         return n;
+    }();
+    static const int env_pcu = [] {                           // A/B runs: this many per CU (<= occupancy)
+        const char* e = getenv("DPF_FOLD_PER_CU");
+        return e && atoi(e) > 0 ? atoi(e) : 0;
     }();
     const uint64_t cap = g_fold_blocks.load(std::memory_order_relaxed);
     const uint64_t msg = (uint64_t)fold_max_sg() / SG * SG > 0 ? (uint64_t)fold_max_sg() / SG * SG : SG;
@@ -1368,8 +1370,16 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
     // combine and less per-workgroup overhead (r05, tools/r05_fpercu.sh,
     // profiles/r05/fold_blocks/, medians of 5: 2^21 x 32 B 22.6 vs 24.7 us,
     // 2^22 34.8 vs 36.0, B = 16 at 2^24 91.9 vs 96.6, B = 32 96.3 vs 99.8;
-    // but B = 64 at 2^23 / 2^24 67.9 / 130.7 vs 67.0 / 125.9).
-    const uint64_t pcu = (!ntdb || MT == 1) && per_cu > 2 ? 2 : (uint64_t)per_cu;
+    // but B = 64 at 2^23 / 2^24 67.9 / 130.7 vs 67.0 / 125.9).  One per CU
+    // for 33-64 keys over a slice of <= 64 MiB (the PIR rank at N = 8): rank
+    // step 0.0741-0.0750 vs 0.0742-0.0759 ms, lower in 5 of 6 interleaved
+    // pairs; at N = 4 (128 MiB) the pairs split 3 / 3 and the fold alone was
+    // slower (37.6 vs 33.9 us), so it keeps 2 (tools/r05_fpercu1.sh,
+    // profiles/r05/fold_blocks/per_cu1_*.txt).
+    const bool small_slice = nsg * 256 * 32 <= (64ull << 20);
+    uint64_t pcu = small_slice && MT == 2 ? 1 : (!ntdb || MT == 1) && per_cu > 2 ? 2 : (uint64_t)per_cu;
+    if (env_pcu > 0) pcu = (uint64_t)(env_pcu < per_cu ? env_pcu : per_cu);
+    if (pcu > (uint64_t)per_cu) pcu = (uint64_t)per_cu;
     const uint64_t resident = (uint64_t)cu_count_fold() * pcu;
     for (uint64_t S0 = 0; S0 < nsg; S0 += per_pass) {
         const uint64_t n = nsg - S0 < per_pass ? nsg - S0 : per_pass;
