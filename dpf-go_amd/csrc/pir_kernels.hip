@@ -561,7 +561,17 @@ __global__ __launch_bounds__(256) void k_xor_parts(const uint32_t* __restrict__ 
 // XOR nparts workgroup partials into the answers (stream-ordered after the fold).
 static hipError_t launch_xor_parts(const uint32_t* parts, uint64_t nparts, uint32_t nkeys, uint32_t pkeys,
                                    uint32_t pwords, uint32_t* ans, uint64_t ans_words, uint32_t off, hipStream_t st) {
-    const uint32_t ys = (uint32_t)(nparts < 64 ? nparts : 64);
+    // Part slices per answer word, one atomic each: 16 for <= 256 partials
+    // (the PIR rank at N = 8: step 0.0733-0.0737 vs 0.0740-0.0745 ms with 64,
+    // 8 in between), 64 above (one GPU, 768 partials: 0.3799-0.3802 vs
+    // 0.3811-0.3817 with 16); tools/r05_xys.sh, profiles/r05/xor_parts/.
+    // DPF_XOR_PARTS_YS=<n> (measurement only) fixes it.
+    static const uint64_t yenv = [] {
+        const char* e = getenv("DPF_XOR_PARTS_YS");
+        return e && atoi(e) > 0 ? (uint64_t)atoi(e) : 0ull;
+    }();
+    const uint64_t ymax = yenv ? yenv : nparts <= 256 ? 16 : 64;
+    const uint32_t ys = (uint32_t)(nparts < ymax ? nparts : ymax);
     hipLaunchKernelGGL(k_xor_parts, dim3((nkeys * pwords + 255) / 256, ys), dim3(256), 0, st, parts, nparts, nkeys,
                        pkeys, pwords, ans, ans_words, off);
     return hipGetLastError();
