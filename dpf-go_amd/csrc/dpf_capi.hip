@@ -936,6 +936,8 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     const uint32_t stop = stop_of(logN);
     const size_t ekb = pir_ek_bytes(nkeys, logN);
     if (work_bytes < nkeys * dpfk::ek_words(stop) * 4) return fail(DPF_ERR_PARAM, "dpf: Eval workspace too small");
+    if (d_xs == nullptr || d_out == nullptr || d_keys == nullptr || (reinterpret_cast<uintptr_t>(d_xs) & 7u) != 0)
+        return fail(DPF_ERR_PARAM, "dpf: d_keys/d_xs/d_out must be device pointers, d_xs 8-byte aligned");
     DeviceGuard g(device);
     forget_expanded(d_work);
     HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop, (uint32_t*)d_work, (hipStream_t)stream));
@@ -1043,9 +1045,11 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
 // PIR kernel over the sliced DB: the tree launch then the fold launch
 // (DPF_PIR_SPLIT, the default: measured faster), or both in one launch
 // where it applies (DPF_PIR_FUSED, k_pir_fused).  DPF_PIR_KERNEL=split|
-// fused|fused-any sets the start value.
+// fused|fused-any sets the start value; in a build without k_pir_fused the
+// environment value falls back to split, as dpf_set_pir_kernel refuses it.
 std::atomic<int> g_pir_kernel{[] {
     const char* e = getenv("DPF_PIR_KERNEL");
+    if (!dpfk::pir_fused_built()) return DPF_PIR_SPLIT;
     if (e && strcmp(e, "fused-any") == 0) return DPF_PIR_FUSED_ANY;
     if (e && e[0] == 'f') return DPF_PIR_FUSED;
     return DPF_PIR_SPLIT;
@@ -1054,7 +1058,7 @@ std::atomic<int> g_pir_kernel{[] {
 int dpf_set_pir_kernel(int kernel) {
     if (kernel != DPF_PIR_SPLIT && kernel != DPF_PIR_FUSED && kernel != DPF_PIR_FUSED_ANY)
         return fail(DPF_ERR_PARAM, "dpf: unknown PIR kernel");
-    if (kernel != DPF_PIR_SPLIT && !dpfk::pir_fused_ok(1, 17, 0, true))
+    if (kernel != DPF_PIR_SPLIT && !dpfk::pir_fused_built())
         return fail(DPF_ERR_PARAM, "dpf: the fused PIR kernel is not in this build (make -C dpf-go_amd experimental)");
     return g_pir_kernel.exchange(kernel);
 }

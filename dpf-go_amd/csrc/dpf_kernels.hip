@@ -1406,7 +1406,12 @@ hipError_t launch_eval(const uint32_t* ek, uint32_t stop, uint32_t logN, const u
         const char* e = getenv("DPF_EVAL_PERSIST");
         return e && *e ? atoi(e) : DPF_EVAL_PERSIST;
     }();
-    if (persist && L > 0 && pts_per_key % 128 == 0 && nq == nkeys * pts_per_key && nq >= 2 * (uint64_t)kEvalPBlock) {
+    // Its LDS-DMA stages a pair's two points with one 16-byte load from xs + 2*pair,
+    // so it needs a 16-byte-aligned xs; an 8-byte-aligned one (a torch slice
+    // xs[1:]) takes k_eval2, whose loads are 8 bytes wide.
+    const bool xs16 = (reinterpret_cast<uintptr_t>(xs) & 15u) == 0;
+    if (persist && xs16 && L > 0 && pts_per_key % 128 == 0 && nq == nkeys * pts_per_key &&
+        nq >= 2 * (uint64_t)kEvalPBlock) {
         const uint64_t want = (nq / 2 + kEvalPBlock - 1) / kEvalPBlock;
         const uint64_t cus = (uint64_t)cu_count();
         hipLaunchKernelGGL(k_eval_persist, dim3((uint32_t)(want < cus ? want : cus)), dim3(kEvalPBlock), 0, st, ek, stop,

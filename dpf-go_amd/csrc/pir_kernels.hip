@@ -604,8 +604,13 @@ void set_fold_limits(uint32_t max_blocks, uint32_t max_sg) {
 namespace {
 
 // Split nchunks into `blocks` contiguous ranges of whole `gran`-chunk batches.
-void split_chunks(uint64_t nchunks, uint64_t want_blocks, uint64_t gran, uint64_t& blocks, uint64_t& cpb) {
-    const uint64_t cap = g_fold_blocks.load(std::memory_order_relaxed);
+// cap_in: the workgroup cap the caller sized its passes with (0: read it
+// here); a launcher that derives a per-workgroup bound from the cap must pass
+// the value it read, so a concurrent dpf_set_fold_limits cannot change it
+// between the two reads.
+void split_chunks(uint64_t nchunks, uint64_t want_blocks, uint64_t gran, uint64_t& blocks, uint64_t& cpb,
+                  uint64_t cap_in = 0) {
+    const uint64_t cap = cap_in ? cap_in : g_fold_blocks.load(std::memory_order_relaxed);
     if (want_blocks > cap) want_blocks = cap;
     cpb = (nchunks + want_blocks - 1) / want_blocks;
     cpb = (cpb + gran - 1) / gran * gran;
@@ -1421,7 +1426,8 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
 #endif
         if (!done) {
             uint64_t spb;
-            split_chunks(n, want, SG, blocks, spb);
+            split_chunks(n, want, SG, blocks, spb, cap);
+            if (spb > msg) return hipErrorInvalidValue;    // fp32-exact counts: never more than msg per workgroup
             if (sgm_keys && sgm_g == 4)
                 hipLaunchKernelGGL((k_fold_mfma<MT, NT, SG, KG, 4>), dim3((uint32_t)blocks), dim3(64 * NW), 0, st, b,
                                    wpk, reinterpret_cast<const uint4*>(d), n, nk, spb, parts, z, zw, wlim, sgm_keys);
@@ -1842,6 +1848,8 @@ __global__ __launch_bounds__(kFzThreads, 1) void k_pir_fused(const uint32_t* __r
         }
 }
 
+bool pir_fused_built() { return true; }
+
 bool pir_fused_ok(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits, bool any_size) {
     if (nkeys == 0 || nkeys > 64 || stop < kFzBlockLog + 1 + prefix_bits) return false;
     const uint32_t wl = stop - 1 - kFzBlockLog - prefix_bits;   // log2 workgroups
@@ -1879,6 +1887,7 @@ hipError_t launch_pir_fused(const uint32_t* ek, uint32_t nkeys, uint32_t stop, u
 
 #else
 bool pir_fused_ok(uint64_t, uint32_t, uint32_t, bool) { return false; }
+bool pir_fused_built() { return false; }
 hipError_t launch_pir_fused(const uint32_t*, uint32_t, uint32_t, uint32_t, uint64_t, const uint8_t*, uint64_t, uint32_t*,
                             uint32_t*, hipStream_t) {
     return hipErrorInvalidValue;

@@ -55,6 +55,8 @@ void set_fold_limits(uint32_t max_blocks, uint32_t max_sg);
 // (make experimental): measured slower than the two launches;
 // otherwise pir_fused_ok() is false and the launcher refuses.
 bool pir_fused_ok(uint64_t nkeys, uint32_t stop, uint32_t prefix_bits, bool any_size = false);
+// Whether k_pir_fused is compiled into this library (the experimental build only).
+bool pir_fused_built();
 hipError_t launch_pir_fused(const uint32_t* ek, uint32_t nkeys, uint32_t stop, uint32_t prefix_bits, uint64_t prefix,
                             const uint8_t* dbs, uint64_t nrec, uint32_t* ans, uint32_t* parts, hipStream_t st);
 

@@ -130,7 +130,10 @@ int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t key_len, 
  * dpf_eval_workspace_size(nkeys, pts_per_key, logN) bytes the queries of a
  * key share its top tree levels (a frontier of 2^L nodes per key computed
  * once); with only dpf_workspace_size(nkeys, logN) bytes each query walks
- * from the root.  Results are identical either way. */
+ * from the root.  Results are identical either way.  d_xs must be 8-byte
+ * aligned (DPF_ERR_PARAM otherwise); a 16-byte-aligned d_xs lets the
+ * persistent kernel stage query pairs by LDS-DMA, an 8-byte-aligned one
+ * (e.g. a tensor slice xs[1:]) runs the per-pair kernel, same results. */
 size_t dpf_eval_workspace_size(size_t nkeys, size_t pts_per_key, uint32_t logN);
 /* Depth L of that shared frontier (0: none).  Work with the frontier:
  * 2^(L+1)-2 AES per key for the frontier nodes, then logN-7-L+1 per query

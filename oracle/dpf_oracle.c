@@ -384,6 +384,68 @@ void oracle_eval_batch(const uint8_t* keys, size_t klen, size_t nkeys, const uin
     run_jobs(&j, eval_worker);
 }
 
+/* EvalFull of one key on nthreads threads, for the full-size parity checks
+ * (configs[3]: logN = 32, 512 MiB).  The DFS (dpf.go:213-241) visits left
+ * before right, so the output is the concatenation of the 2^d subtrees at
+ * depth d in prefix order.  Thread j takes subtrees j, j+n, ...: it walks the
+ * root to subtree p's root with the same per-level step evalFullRecursive
+ * applies (prg + CW under t, :229-238, child chosen by bit d-1-i of p) and
+ * then runs the recursion from level d into the subtree's slice of out. */
+typedef struct {
+    mmo_fn f;
+    const uint8_t* key; size_t klen; uint64_t logN; uint8_t* out;
+    int depth, nthreads, tid;
+} sub_job_t;
+
+static void* evalfull_sub_worker(void* p) {
+    sub_job_t* j = (sub_job_t*)p;
+    uint64_t stop = stop_of(j->logN);
+    size_t part = oracle_out_len(j->logN) >> j->depth;
+    block_t stack[64][2];
+    for (uint64_t pre = (uint64_t)j->tid; pre < ((uint64_t)1 << j->depth); pre += (uint64_t)j->nthreads) {
+        block_t s, sL, sR;
+        memcpy(s, j->key, 16);
+        uint8_t t = j->key[16];
+        for (int i = 0; i < j->depth; ++i) {
+            uint8_t tL, tR;
+            prg(j->f, s, sL, sR, &tL, &tR);
+            if (t != 0) {
+                const uint8_t* sCW = j->key + 17 + (size_t)i * 18;
+                xor16(sL, sL, sCW);
+                xor16(sR, sR, sCW);
+                tL ^= j->key[17 + i * 18 + 16];
+                tR ^= j->key[17 + i * 18 + 17];
+            }
+            if ((pre >> (j->depth - 1 - i)) & 1) { memcpy(s, sR, 16); t = tR; }
+            else                                 { memcpy(s, sL, 16); t = tL; }
+        }
+        bytearr b = {j->out + pre * part, 0};
+        eval_full_rec(j->f, stack, j->key, j->klen, s, t, (uint64_t)j->depth, stop, &b);
+    }
+    return NULL;
+}
+
+void oracle_evalfull_mt(const uint8_t* key, size_t klen, uint64_t logN, uint8_t* out, int nthreads,
+                        int use_aesni) {
+    mmo_fn f = pick_mmo(use_aesni);
+    uint64_t stop = stop_of(logN);
+    int n = nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads);
+    int depth = 0;
+    while (depth < 8 && (uint64_t)depth < stop && (1 << depth) < 4 * n) ++depth;
+    memset(out, 0, oracle_out_len(logN));
+    if (depth == 0) { evalfull_with(f, key, klen, logN, out); return; }
+    if (n > (1 << depth)) n = 1 << depth;
+    pthread_t th[256];
+    sub_job_t jobs[256];
+    for (int i = 0; i < n; ++i) {
+        sub_job_t jj = {f, key, klen, logN, out, depth, n, i};
+        jobs[i] = jj;
+    }
+    for (int i = 1; i < n; ++i) pthread_create(&th[i], NULL, evalfull_sub_worker, &jobs[i]);
+    evalfull_sub_worker(&jobs[0]);
+    for (int i = 1; i < n; ++i) pthread_join(th[i], NULL);
+}
+
 /* PIR answer (build-only operator, SURVEY §8a last row): XOR of the 32-byte
  * DB records whose EvalFull bit is set.  Records [rec_lo, rec_lo+nrec). */
 void oracle_pir_answer(const uint8_t* key, size_t klen, uint64_t logN, const uint8_t* db,
@@ -398,4 +460,57 @@ void oracle_pir_answer(const uint8_t* key, size_t klen, uint64_t logN, const uin
             for (int b = 0; b < 32; ++b) ans[b] ^= db[i * 32 + b];
     }
     free(bits);
+}
+
+/* The same answer for a batch of keys, split into nslices equal record
+ * slices of the domain (slice s = records [s*2^logN/nslices, (s+1)*...) of
+ * the DB, cut at nrec): ans[k][s][32] is key k's partial over slice s, the
+ * value an N = nslices PIR rank returns; XOR over s gives oracle_pir_answer.
+ * Keys are split over nthreads threads; each key's EvalFull bits
+ * (dpf.go:243-262, AES-NI restatement) select records by a 64-bit mask
+ * instead of a branch, XORed 8 bytes at a time. */
+typedef struct {
+    const uint8_t* keys; size_t klen; size_t nkeys; uint64_t logN;
+    const uint8_t* db; uint64_t nrec; int nslices; uint8_t* ans; int nthreads, tid;
+} pir_job_t;
+
+static void* pir_worker(void* p) {
+    pir_job_t* j = (pir_job_t*)p;
+    size_t ol = oracle_out_len(j->logN);
+    uint8_t* bits = (uint8_t*)malloc(ol);
+    uint64_t dom = j->logN >= 64 ? ~(uint64_t)0 : ((uint64_t)1 << j->logN);
+    uint64_t per = dom / (uint64_t)j->nslices;
+    for (size_t k = (size_t)j->tid; k < j->nkeys; k += (size_t)j->nthreads) {
+        evalfull_with(pick_mmo(1), j->keys + k * j->klen, j->klen, j->logN, bits);
+        for (int s = 0; s < j->nslices; ++s) {
+            uint64_t lo = (uint64_t)s * per, hi = lo + per;
+            if (hi > j->nrec) hi = j->nrec;
+            uint64_t acc[4] = {0, 0, 0, 0};
+            for (uint64_t x = lo; x < hi; ++x) {
+                uint64_t m = (uint64_t)0 - (uint64_t)((bits[x >> 3] >> (x & 7)) & 1);
+                uint64_t r[4];
+                memcpy(r, j->db + x * 32, 32);
+                acc[0] ^= r[0] & m; acc[1] ^= r[1] & m; acc[2] ^= r[2] & m; acc[3] ^= r[3] & m;
+            }
+            memcpy(j->ans + (k * (size_t)j->nslices + (size_t)s) * 32, acc, 32);
+        }
+    }
+    free(bits);
+    return NULL;
+}
+
+void oracle_pir_answer_batch(const uint8_t* keys, size_t klen, size_t nkeys, uint64_t logN, const uint8_t* db,
+                             uint64_t nrec, int nslices, uint8_t* ans, int nthreads) {
+    oracle_init();
+    int n = nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads);
+    if (nslices < 1) nslices = 1;
+    pthread_t th[256];
+    pir_job_t jobs[256];
+    for (int i = 0; i < n; ++i) {
+        pir_job_t jj = {keys, klen, nkeys, logN, db, nrec, nslices, ans, n, i};
+        jobs[i] = jj;
+    }
+    for (int i = 1; i < n; ++i) pthread_create(&th[i], NULL, pir_worker, &jobs[i]);
+    pir_worker(&jobs[0]);
+    for (int i = 1; i < n; ++i) pthread_join(th[i], NULL);
 }

@@ -50,6 +50,9 @@ def lib() -> ctypes.CDLL:
                                         ctypes.c_uint64, _u8p, ctypes.c_int, ctypes.c_int]
         L.oracle_pir_answer.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_uint64, _u8p, ctypes.c_uint64,
                                         ctypes.c_uint64, _u8p]
+        L.oracle_evalfull_mt.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_uint64, _u8p, ctypes.c_int, ctypes.c_int]
+        L.oracle_pir_answer_batch.argtypes = [_u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, _u8p,
+                                              ctypes.c_uint64, ctypes.c_int, _u8p, ctypes.c_int]
         L.oracle_init()
         _lib = L
     return _lib
@@ -113,6 +116,15 @@ def evalfull(key: bytes, logN: int, aesni: bool = False) -> bytes:
     return out.tobytes()
 
 
+def evalfull_mt(key: bytes, logN: int, nthreads: int = 16, aesni: bool = True) -> np.ndarray:
+    """EvalFull of one key split over depth-d subtrees on nthreads threads
+    (the DFS output is their concatenation in prefix order) -> uint8 array."""
+    k = _u8(key)
+    out = np.empty(out_len(logN), np.uint8)
+    lib().oracle_evalfull_mt(_p(k), k.size, logN, _p(out), nthreads, int(aesni))
+    return out
+
+
 def evalfull_batch(keys: np.ndarray, logN: int, nthreads: int = 1, aesni: bool = True) -> np.ndarray:
     kk = np.ascontiguousarray(keys, dtype=np.uint8)
     n, kl = kk.shape
@@ -137,3 +149,17 @@ def pir_answer(key: bytes, logN: int, db: np.ndarray, rec_lo: int, nrec: int) ->
     ans = np.zeros(32, np.uint8)
     lib().oracle_pir_answer(_p(k), k.size, logN, _p(d), rec_lo, nrec, _p(ans))
     return ans.tobytes()
+
+
+def pir_answer_batch(keys: np.ndarray, logN: int, db: np.ndarray, nrec: int, nslices: int = 1,
+                     nthreads: int = 16) -> np.ndarray:
+    """Every key's XOR inner product over the DB, split into nslices equal
+    record slices of the domain -> uint8[nkeys, nslices, 32]; the slice
+    partials are what an N = nslices PIR rank returns, their XOR the answer."""
+    kk = np.ascontiguousarray(keys, dtype=np.uint8)
+    n, kl = kk.shape
+    d = np.ascontiguousarray(db, dtype=np.uint8).reshape(-1)
+    assert d.size >= nrec * 32
+    ans = np.zeros((n, nslices, 32), np.uint8)
+    lib().oracle_pir_answer_batch(_p(kk), kl, n, logN, _p(d), nrec, nslices, _p(ans), nthreads)
+    return ans

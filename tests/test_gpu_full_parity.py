@@ -1,0 +1,143 @@
+"""Full-size parity: every output byte of BASELINE configs[1] and configs[3],
+on the bench's own keys, against the CPU oracle (VERDICT r05 "Next" #1).
+
+The share-XOR property used before at these sizes cannot see an error off
+the alpha path: there both shares carry the same seeds and t bytes, so a
+deterministic kernel fault corrupts both identically and cancels.  Here
+nothing is sampled:
+
+  - configs[1] (4096 keys x logN=20, 512 MiB per share), bench.py's rank-0
+    keys (synth seed, first=0): both shares, both AES back ends, through the
+    device entry point bench.py times (dpf_evalfull_batch_dev) and once
+    through the host-buffer C ABI (dpf_evalfull_batch, chunked pipeline);
+  - configs[3] (one key, logN=32, 512 MiB), bench.py's key (first=777):
+    both shares, both back ends, the whole output of dpf_evalfull_batch_dev
+    and the 8 prefix-3 subtree slices of the N = 8 ranks
+    (dpf_evalfull_subtree_dev) reassembled.
+
+Reference: EvalFull /root/reference/dpf/dpf.go:243-262 (evalFullRecursive
+:213-241, left before right).  The oracle is oracle/dpf_oracle.c
+(oracle_evalfull_batch / oracle_evalfull_mt, AES-NI restatement).
+"""
+import numpy as np
+import pytest
+
+import dpf
+from dpf import synth
+import oracle
+
+pytestmark = pytest.mark.gpu
+NT = 16          # the GPU box's CPU share
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert dpf.gpu_init(1) >= 1
+    prev = dpf.set_small_call_path("gpu")
+    yield
+    dpf.set_small_call_path(prev)
+
+
+def _stream():
+    import torch
+    return torch.cuda.current_stream(torch.device("cuda", 0))
+
+
+@pytest.fixture(scope="module")
+def cfg1():
+    """bench.py's configs[1] keys (rank 0) and their oracle EvalFull, both shares."""
+    logN, nk = 20, 4096
+    al, s0, s1 = synth.key_seeds(nk, logN, first=0)
+    ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+    want = {"a": oracle.evalfull_batch(ka, logN, nthreads=NT), "b": oracle.evalfull_batch(kb, logN, nthreads=NT)}
+    return logN, al, {"a": ka, "b": kb}, want
+
+
+def _dev_evalfull(keys: np.ndarray, logN: int) -> np.ndarray:
+    import torch
+    dev = torch.device("cuda", 0)
+    nk, kl = keys.shape
+    ol = dpf.evalfull_len(logN)
+    d_keys = torch.from_numpy(keys.reshape(-1).copy()).to(dev)
+    d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=dev)
+    d_out = torch.empty(nk * ol, dtype=torch.uint8, device=dev)
+    d_out.fill_(0x5A)                         # every byte must be written
+    dpf.evalfull_batch_dev(d_keys, kl, nk, logN, d_out, d_work, stream=_stream())
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy().reshape(nk, ol)
+    dpf.forget_workspace(d_work)
+    return out
+
+
+def _first_diff(got: np.ndarray, want: np.ndarray) -> str:
+    bad = np.argwhere(got != want)
+    return f"{bad.shape[0]} bytes differ, first at {tuple(bad[0])}" if bad.size else "equal"
+
+
+@pytest.mark.parametrize("aes", ["ttable", "bitsliced"])
+@pytest.mark.parametrize("share", ["a", "b"])
+def test_config1_every_byte_vs_oracle(cfg1, aes, share):
+    logN, al, keys, want = cfg1
+    prev = dpf.set_aes_impl(aes)
+    try:
+        got = _dev_evalfull(keys[share], logN)
+    finally:
+        dpf.set_aes_impl(prev)
+    assert np.array_equal(got, want[share]), _first_diff(got, want[share])
+
+
+def test_config1_host_buffer_api_every_byte(cfg1):
+    """The drop-in host-buffer entry (dpf_evalfull_batch: staged chunks,
+    kernel / D2H / host copy overlapped) at full size."""
+    logN, al, keys, want = cfg1
+    got = dpf.evalfull_batch(keys["a"], logN, ngpus=1)
+    assert np.array_equal(got, want["a"]), _first_diff(got, want["a"])
+    x = np.unpackbits(want["a"][:64] ^ want["b"][:64], axis=1, bitorder="little")
+    assert (x.sum(axis=1) == 1).all() and all(x[i, int(al[i])] for i in range(64))
+
+
+@pytest.fixture(scope="module")
+def cfg3():
+    """bench.py's configs[3] key (first=777), both shares, and the oracle's
+    whole logN=32 EvalFull of each (512 MiB, threaded over subtrees)."""
+    logN = 32
+    al, s0, s1 = synth.key_seeds(1, logN, first=777)
+    ka, kb = dpf.gen_seeded(int(al[0]), logN, s0[0].tobytes(), s1[0].tobytes())
+    want = {"a": oracle.evalfull_mt(ka, logN, nthreads=NT), "b": oracle.evalfull_mt(kb, logN, nthreads=NT)}
+    x = np.bitwise_xor(want["a"].view(np.uint64), want["b"].view(np.uint64))
+    nz = np.flatnonzero(x)
+    assert nz.size == 1 and int(nz[0]) * 64 + int(x[nz[0]]).bit_length() - 1 == int(al[0])
+    return logN, {"a": ka, "b": kb}, want
+
+
+@pytest.mark.parametrize("aes", ["ttable", "bitsliced"])
+@pytest.mark.parametrize("share", ["a", "b"])
+def test_config3_every_byte_vs_oracle(cfg3, aes, share):
+    import torch
+    logN, keys, want = cfg3
+    key = keys[share]
+    dev = torch.device("cuda", 0)
+    kl, ol, pb = len(key), dpf.evalfull_len(logN), 3
+    part = ol >> pb
+    w = torch.from_numpy(want[share]).to(dev)
+    d_key = torch.from_numpy(np.frombuffer(key, np.uint8).copy()).to(dev)
+    d_work = torch.empty(dpf.workspace_size(1, logN), dtype=torch.uint8, device=dev)
+    d_out = torch.empty(ol, dtype=torch.uint8, device=dev)
+    prev = dpf.set_aes_impl(aes)
+    try:
+        d_out.fill_(0x5A)
+        dpf.evalfull_batch_dev(d_key, kl, 1, logN, d_out, d_work, stream=_stream())
+        torch.cuda.synchronize()
+        ne = int((d_out != w).sum())
+        assert ne == 0, f"whole output: {ne} bytes differ"
+        # the N = 8 ranks' slices (subtree r at depth 3), into their offsets
+        d_out.fill_(0xA5)
+        for r in range(1 << pb):
+            dpf.evalfull_subtree_dev(d_key, kl, 1, logN, pb, r, d_out[r * part:(r + 1) * part], d_work,
+                                     stream=_stream())
+        torch.cuda.synchronize()
+        ne = int((d_out != w).sum())
+        assert ne == 0, f"8 subtree slices: {ne} bytes differ"
+    finally:
+        dpf.set_aes_impl(prev)
+        dpf.forget_workspace(d_work)

@@ -222,14 +222,20 @@ def test_logN32_single_key_property():
 
 @pytest.mark.parametrize("logN,nk,ppk", [(13, 8, 256), (14, 5, 1000), (20, 6, 1024), (20, 3, 3000), (32, 4, 512),
                                          (63, 2, 700), (15, 3, 257), (20, 600, 1024), (17, 2100, 128),
-                                         (20, 8, 256), (21, 8, 256)])
+                                         (20, 8, 256), (21, 8, 256), (22, 8, 256)])
 def test_eval_frontier_path_vs_oracle(logN, nk, ppk):
     """Shared-frontier Eval kernel (taken when a key has >= 256 points).
     (20, 600, 1024) gives the persistent kernel two ragged passes over its
     resident threads; (17, 2100, 128) one partial pass.  The persistent
-    kernel stages a pair's key records in LDS when they fit 64 words:
-    (20, 8, 256) is the largest such walk (7 levels + final CW = 60 words),
-    (21, 8, 256) and (32, 4, 512) take the scalar-load walk."""
+    kernel stages a pair's key records in LDS when they fit 64 words
+    (one 8-word record per level below the frontier level L, + 4 for
+    the final CW): at
+    ppk = 256, L = 7, so (20, 8, 256) stages 6*8+4 = 52 words and
+    (21, 8, 256) 7*8+4 = 60, the largest LDS-staged walk; (22, 8, 256)
+    needs 68, the first size past the limit, and takes the scalar-load
+    walk, as does (32, 4, 512)."""
+    if ppk == 256 and logN in (20, 21, 22):
+        assert dpf.eval_frontier_level(logN, ppk) == 7
     _, ka, _ = _keys(nk, logN, first=8000 + logN + ppk)
     xs = synth.eval_points(nk, ppk, logN)
     xs[:, 0] = 0
@@ -293,3 +299,34 @@ def test_tiny_domains_all_points(logN):
         assert np.array_equal(dpf.evalfull_batch(k, logN, ngpus=1), oracle.evalfull_batch(k, logN, nthreads=1))
     got = dpf.eval_batch(ka, xs, logN, ngpus=1) ^ dpf.eval_batch(kb, xs, logN, ngpus=1)
     assert np.array_equal(got, (xs == al[:, None]).astype(np.uint8))
+
+
+def test_eval_dev_points_at_8_byte_offset():
+    """the persistent Eval kernel loads a pair's two points with
+    one 16-byte LDS-DMA, so a d_xs that is only 8-byte aligned (a tensor
+    slice xs[1:]) must take the per-pair kernel and give the same answers;
+    a d_xs that is not 8-byte aligned is rejected."""
+    import torch
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    logN, nk, ppk = 20, 64, 1024              # persistent shape (frontier, wave-uniform keys)
+    _, ka, _ = _keys(nk, logN, first=6060)
+    xs = synth.eval_points(nk, ppk, logN, master=0xA11)
+    kl = dpf.key_len(logN)
+    d_keys = torch.from_numpy(ka.reshape(-1)).to(dev)
+    d_xs_big = torch.zeros(nk * ppk + 2, dtype=torch.int64, device=dev)
+    d_xs_big[1:1 + nk * ppk] = torch.from_numpy(xs.reshape(-1).view(np.int64)).to(dev)
+    d_xs = d_xs_big[1:1 + nk * ppk]
+    assert d_xs.data_ptr() % 16 == 8
+    d_work = torch.empty(dpf.eval_workspace_size(nk, ppk, logN), dtype=torch.uint8, device=dev)
+    d_out = torch.empty(nk * ppk, dtype=torch.uint8, device=dev)
+    dpf.eval_batch_dev(d_keys, kl, nk, d_xs, ppk, logN, d_out, d_work, stream=st)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy().reshape(nk, ppk), oracle.eval_batch(ka, xs, logN, nthreads=NT))
+    raw = torch.zeros(nk * ppk * 8 + 16, dtype=torch.uint8, device=dev)
+    with pytest.raises(dpf.DPFPanic) as e:
+        dpf.lib()  # noqa: B018
+        rc = dpf.lib().dpf_eval_batch_dev(0, d_keys.data_ptr(), kl, nk, raw.data_ptr() + 3, ppk, logN,
+                                          d_out.data_ptr(), d_work.data_ptr(), d_work.numel(), st.cuda_stream)
+        dpf._check(rc)
+    assert e.value.code == dpf.DPF_ERR_PARAM

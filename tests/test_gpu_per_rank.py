@@ -99,19 +99,18 @@ def test_config3_eight_prefix3_subtrees_of_one_logN32_key(aes):
         dpf.set_aes_impl(prev)
 
 
-def test_config4_eight_db_slices_logN24():
-    """configs[4] per rank at N=8, all 8 ranks in turn on one GPU, B=64."""
+def test_config4_eight_db_slices_logN24(cfg4):
+    """configs[4] per rank at N=8 over the row-major DB (dpf_pir_answer_dev),
+    all 8 ranks in turn on one GPU, B=64: every key's partial of both
+    servers vs the oracle's slice partial."""
     import torch
     logN, pb, nk = 24, 3, 64
-    nrec = 1 << logN
-    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
-    al, s0, s1 = synth.key_seeds(nk, logN, first=4242)
-    ka, kb = dpf.gen_batch_seeded(al, logN, s0, s1)
+    nrec, db, al, ka, kb = cfg4["nrec"], cfg4["db"], cfg4["al"], cfg4["ka"], cfg4["kb"]
     kl = dpf.key_len(logN)
     dev = torch.device("cuda", 0)
     d_ka = torch.from_numpy(ka.reshape(-1)).to(dev)
     d_kb = torch.from_numpy(kb.reshape(-1)).to(dev)
-    d_db = torch.from_numpy(db.reshape(-1)).to(dev)
+    d_db = cfg4["d_db"]
     d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=dev)
     # the 1-GPU answer over the whole DB
     d_work = torch.empty(dpf.pir_workspace_size(nk, logN, 0), dtype=torch.uint8, device=dev)
@@ -130,9 +129,10 @@ def test_config4_eight_db_slices_logN24():
                                stream=_stream())
             torch.cuda.synchronize()
             parts.append(d_ans.cpu().numpy().reshape(nk, 32).copy())
-        for i in (0, nk - 1):
-            want = np.frombuffer(oracle.pir_answer(ka[i].tobytes(), logN, db[lo:hi], lo, hi - lo), np.uint8)
-            assert np.array_equal(parts[0][i], want), (r, i)
+        for j, share in enumerate(("a", "b")):
+            want = cfg4["oracle_" + share][:, r, :]
+            bad = np.argwhere(parts[j] != want)
+            assert bad.size == 0, (share, r, f"first differing key {bad[0][0]}" if bad.size else "")
         acc_a ^= parts[0]
         acc_b ^= parts[1]
     assert np.array_equal(acc_a, whole_a)
@@ -166,8 +166,16 @@ def cfg4():
         whole.append(d_ans.cpu().numpy().reshape(nk, 32).copy())
     dpf.forget_workspace(d_work)
     del d_dbs, d_work
+    # The oracle's partial of every key over each of the 8 rank slices (an
+    # N = 2 / 4 rank's partial is the XOR of 4 / 2 consecutive ones).
+    ora = {"a": oracle.pir_answer_batch(ka, logN, db, nrec, nslices=8),
+           "b": oracle.pir_answer_batch(kb, logN, db, nrec, nslices=8)}
+    for j, share in enumerate(("a", "b")):
+        want = np.bitwise_xor.reduce(ora[share], axis=1)
+        bad = np.argwhere(whole[j] != want)
+        assert bad.size == 0, (share, f"1-GPU answer of key {bad[0][0]} differs" if bad.size else "")
     return {"logN": logN, "nk": nk, "nrec": nrec, "db": db, "al": al, "ka": ka, "kb": kb, "d_db": d_db,
-            "whole_a": whole[0], "whole_b": whole[1]}
+            "whole_a": whole[0], "whole_b": whole[1], "oracle_a": ora["a"], "oracle_b": ora["b"]}
 
 
 @pytest.mark.parametrize("pb", [1, 2, 3])
@@ -177,9 +185,10 @@ def test_config4_sliced_product_path_per_rank(cfg4, pb):
     [r*2^(24-pb), (r+1)*2^(24-pb)) once (dpf_pir_db_slice_dev on d_db[lo:hi])
     and answers with dpf_pir_answer_sliced_dev(prefix_bits=pb, prefix=r):
     subtree r of every key (dpf/dpf.go:213-241 below the prefix) folded on the
-    matrix cores.  Keys 0 and 63 of every rank vs the oracle's XOR inner
-    product over that slice (dpf.go:243-262 bits), the partials XOR to the
-    1-GPU sliced answer, and the two servers XOR to DB[alpha]."""
+    matrix cores.  The partials XOR to the
+    1-GPU sliced answer, and the two servers XOR to DB[alpha].  Every key's
+    partial of both servers at every rank against the oracle's partial over
+    that slice (dpf.go:243-262 bits)."""
     import torch
     logN, nk, nrec, db = cfg4["logN"], cfg4["nk"], cfg4["nrec"], cfg4["db"]
     ka, kb, d_db = cfg4["ka"], cfg4["kb"], cfg4["d_db"]
@@ -204,9 +213,11 @@ def test_config4_sliced_product_path_per_rank(cfg4, pb):
                                       prefix=prefix, stream=_stream())
             torch.cuda.synchronize()
             parts.append(d_ans.cpu().numpy().reshape(nk, 32).copy())
-        for i in (0, nk - 1):
-            want = np.frombuffer(oracle.pir_answer(ka[i].tobytes(), logN, db[lo:hi], lo, hi - lo), np.uint8)
-            assert np.array_equal(parts[0][i], want), (r, i)
+        g = 8 // W                                   # oracle slices per rank
+        for j, share in enumerate(("a", "b")):
+            want = np.bitwise_xor.reduce(cfg4["oracle_" + share][:, r * g:(r + 1) * g, :], axis=1)
+            bad = np.argwhere(parts[j] != want)
+            assert bad.size == 0, (share, r, f"first differing key {bad[0][0]}" if bad.size else "")
         acc[0] ^= parts[0]
         acc[1] ^= parts[1]
         del d_dbs
@@ -247,8 +258,8 @@ assert np.array_equal(a8, a1)
 rec = a8 ^ b8
 for i in range(nk):
     assert np.array_equal(rec[i], db[int(al[i])]), i
-for i in (0, nk - 1):
-    assert a8[i].tobytes() == oracle.pir_answer(ka[i].tobytes(), logN, db, 0, nrec), i
+want = oracle.pir_answer_batch(ka, logN, db, nrec, nslices=1)[:, 0, :]
+assert np.array_equal(a8, want), np.argwhere(a8 != want)[:1]
 dpf.gpu_shutdown()
 print("done")
 ''' % (os.path.join(root, "dpf-go_amd"), os.path.join(root, "oracle"))

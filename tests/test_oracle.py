@@ -109,3 +109,27 @@ def test_aesni_and_portable_agree():
     a = oracle.evalfull_batch(keys, 12, nthreads=3, aesni=True)
     b = np.stack([np.frombuffer(oracle.evalfull(k.tobytes(), 12, aesni=False), np.uint8) for k in keys])
     assert np.array_equal(a, b)
+
+
+def test_oracle_threaded_evalfull_and_sliced_pir_match_restatement():
+    """The threaded subtree EvalFull and the batched sliced PIR answer (used
+    by the full-size GPU parity tests) equal the plain restatements."""
+    import numpy as np
+    from dpf import synth
+    for logN in (7, 9, 14):
+        al, s0, s1 = synth.key_seeds(2, logN, first=70 + logN)
+        for i in range(2):
+            ka, _ = oracle.gen(int(al[i]), logN, s0[i].tobytes(), s1[i].tobytes())
+            for nt in (1, 3, 8):
+                assert oracle.evalfull_mt(ka, logN, nt).tobytes() == oracle.evalfull(ka, logN)
+    logN, nrec = 12, (1 << 12) - 77
+    db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+    al, s0, s1 = synth.key_seeds(4, logN, first=9)
+    keys = np.stack([np.frombuffer(oracle.gen(int(al[i]), logN, s0[i].tobytes(), s1[i].tobytes())[0], np.uint8)
+                     for i in range(4)])
+    a = oracle.pir_answer_batch(keys, logN, db, nrec, nslices=8, nthreads=3)
+    for i in range(4):
+        assert np.bitwise_xor.reduce(a[i], axis=0).tobytes() == oracle.pir_answer(keys[i].tobytes(), logN, db, 0, nrec)
+        for s in range(8):
+            lo, hi = s << 9, min(nrec, (s + 1) << 9)
+            assert a[i, s].tobytes() == oracle.pir_answer(keys[i].tobytes(), logN, db[lo:hi], lo, hi - lo)
