@@ -254,6 +254,26 @@ struct DeviceGuard {
     }
 };
 
+// Streams created by dpf_stream_create_cu_masked and the CUs each may use.
+// A _dev entry point launching on one of them sizes its grids to those CUs
+// (CuScope); any other stream gets the whole device.
+std::mutex g_cus_mu;
+std::unordered_map<hipStream_t, int> g_stream_cus;
+
+struct CuScope {
+    int prev;
+    explicit CuScope(void* stream) : prev(dpfk::cu_budget()) {
+        int c = 0;
+        if (stream) {
+            std::lock_guard<std::mutex> lk(g_cus_mu);
+            auto it = g_stream_cus.find((hipStream_t)stream);
+            if (it != g_stream_cus.end()) c = it->second;
+        }
+        dpfk::set_cu_budget(c);
+    }
+    ~CuScope() { dpfk::set_cu_budget(prev); }
+};
+
 Dev::~Dev() {
     std::lock_guard<std::mutex> dl(mu);
     DeviceGuard g(id);
@@ -907,6 +927,7 @@ int dpf_evalfull_subtree_dev(int device, const uint8_t* d_keys, size_t klen, siz
         return fail(DPF_ERR_PARAM, "dpf: subtree prefix out of range");
     if (nkeys == 0) return DPF_OK;
     DeviceGuard g(device);
+    CuScope cus(stream);
     const bool bs = want_bs();
     bool expanded = false;
     forget_expanded(d_work);
@@ -939,6 +960,7 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     if (d_xs == nullptr || d_out == nullptr || d_keys == nullptr || (reinterpret_cast<uintptr_t>(d_xs) & 7u) != 0)
         return fail(DPF_ERR_PARAM, "dpf: d_keys/d_xs/d_out must be device pointers, d_xs 8-byte aligned");
     DeviceGuard g(device);
+    CuScope cus(stream);
     forget_expanded(d_work);
     HIP_TRY(dpfk::launch_unpack(d_keys, klen, nkeys, stop, (uint32_t*)d_work, (hipStream_t)stream));
     // The frontier (if it fits in the rest of the workspace) lets queries share the tree's top levels.
@@ -952,6 +974,7 @@ int dpf_expand_keys_dev(int device, const uint8_t* d_keys, size_t klen, size_t n
                         void* stream) {
     if (int rc = check_key(klen, logN)) return rc;
     DeviceGuard g(device);
+    CuScope cus(stream);
     const bool bs = want_bs();
     forget_expanded(d_work);
     HIP_TRY(expand_keys(d_keys, klen, nkeys, stop_of(logN), tree_ws(d_work, nkeys, stop_of(logN)), (hipStream_t)stream,
@@ -981,6 +1004,7 @@ int dpf_evalfull_expanded_dev(int device, void* d_work, size_t nkeys, uint32_t l
         build_bs = bs && !it->second.bs;
     }
     DeviceGuard g(device);
+    CuScope cus(stream);
     const TreeWs w = tree_ws(d_work, nkeys, stop);
     if (build_bs) {
         HIP_TRY(dpfk::launch_bs_from_ek(w.ek, nkeys, stop, w.ekb, (hipStream_t)stream));
@@ -1022,6 +1046,7 @@ int dpf_pir_answer_dev(int device, const uint8_t* d_keys, size_t klen, size_t nk
     if (nrec > slice) return fail(DPF_ERR_PARAM, "dpf: more DB records than the subtree's domain");
     if (int rc = check_pir_bufs(d_keys, nkeys, d_db, nrec, d_ans, d_work)) return rc;
     DeviceGuard g(device);
+    CuScope cus(stream);
     hipStream_t st = (hipStream_t)stream;
     if (nkeys == 0) return DPF_OK;
     if (nrec == 0) {
@@ -1093,6 +1118,7 @@ int dpf_pir_answer_sliced_dev(int device, const uint8_t* d_keys, size_t klen, si
     if (nrec > slice) return fail(DPF_ERR_PARAM, "dpf: more DB records than the subtree's domain");
     if (int rc = check_pir_bufs(d_keys, nkeys, d_dbs, nrec, d_ans, d_work)) return rc;
     DeviceGuard g(device);
+    CuScope cus(stream);
     hipStream_t st = (hipStream_t)stream;
     if (nkeys == 0) return DPF_OK;
     if (nrec == 0) {
@@ -1134,6 +1160,7 @@ int dpf_xor_fold_sliced_dev(int device, const uint8_t* d_bits, size_t bits_strid
     if (nkeys > 0 && (!d_ans || !d_work || (nrec > 0 && (!d_bits || !d_dbs))))
         return fail(DPF_ERR_PARAM, "dpf: null device buffer");
     DeviceGuard g(device);
+    CuScope cus(stream);
     if (nkeys == 0) return DPF_OK;
     HIP_TRY(dpfk::launch_pir_fold_sliced((const uint32_t*)d_bits, bits_stride / 4, d_dbs, nrec, (uint32_t)nkeys,
                                          (uint32_t*)d_ans, (uint32_t*)d_work, (hipStream_t)stream));
@@ -1157,6 +1184,7 @@ int dpf_xor_fold_dev(int device, const uint8_t* d_bits, size_t bits_stride, size
     if (nkeys > 0 && (!d_ans || !d_work || (nrec > 0 && (!d_bits || !d_payload))))
         return fail(DPF_ERR_PARAM, "dpf: null device buffer");
     DeviceGuard g(device);
+    CuScope cus(stream);
     hipStream_t st = (hipStream_t)stream;
     if (nkeys == 0) return DPF_OK;
     HIP_TRY(dpfk::launch_pir_fold((const uint32_t*)d_bits, bits_stride / 4, d_payload, nrec, rec_bytes, (uint32_t)nkeys,
@@ -1264,5 +1292,35 @@ int dpf_pir_answer(void* handle, const uint8_t* keys, size_t klen, size_t nkeys,
 }
 
 void dpf_pir_db_free(void* handle) { delete (PirDb*)handle; }
+
+int dpf_stream_create_cu_masked(int device, uint32_t cu_first, uint32_t cu_count, void** stream) {
+    if (!stream) return fail(DPF_ERR_PARAM, "dpf: null stream out-pointer");
+    *stream = nullptr;
+    DeviceGuard g(device);
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+    if (cu_count == 0 || (uint64_t)cu_first + cu_count > (uint64_t)ncu)
+        return fail(DPF_ERR_PARAM, "dpf: CU range outside the device");
+    std::vector<uint32_t> mask(((size_t)ncu + 31) / 32, 0u);
+    for (uint32_t b = cu_first; b < cu_first + cu_count; ++b) mask[b / 32] |= 1u << (b % 32);
+    hipStream_t st = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    {
+        std::lock_guard<std::mutex> lk(g_cus_mu);
+        g_stream_cus[st] = (int)cu_count;
+    }
+    *stream = st;
+    return DPF_OK;
+}
+
+int dpf_stream_destroy(void* stream) {
+    if (!stream) return DPF_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_cus_mu);
+        g_stream_cus.erase((hipStream_t)stream);
+    }
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return DPF_OK;
+}
 
 }  // extern "C"

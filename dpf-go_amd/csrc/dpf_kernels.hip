@@ -1153,7 +1153,15 @@ static hipError_t launch_full_d(const uint32_t* ek, uint32_t stop, uint64_t nuni
     return hipGetLastError();
 }
 
-static int cu_count() {
+// CUs a launch may occupy: the calling thread's budget when the C ABI set
+// one (a stream created with a CU mask, dpf_stream_create_cu_masked), else
+// the device's.  Grid shapes (one round of resident waves, the depth model)
+// are sized to it, so a kernel on a 64-CU stream does not queue 4 rounds.
+static thread_local int t_cu_budget = 0;
+void set_cu_budget(int cus) { t_cu_budget = cus; }
+int cu_budget() { return t_cu_budget; }
+int cu_count() {
+    if (t_cu_budget > 0) return t_cu_budget;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

@@ -19,6 +19,12 @@ constexpr int kTreeWaves = DPF_TREE_WAVES;
 constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
 constexpr uint32_t kMaxFrontierHbm = 16;  // batched Eval, HBM frontier: deepest shared level
 
+// CU budget of the calling thread's launches (0: the whole device); see
+// cu_count() in dpf_kernels.hip.
+void set_cu_budget(int cus);
+int cu_budget();
+int cu_count();
+
 // Expanded-key words per key: (stop + 2) records of 8 u32.
 inline uint64_t ek_words(uint32_t stop) { return ((uint64_t)stop + 2) * 8; }
 

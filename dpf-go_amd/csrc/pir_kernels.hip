@@ -35,6 +35,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "dpf_kernels.hpp"
 #include "pir_kernels.hpp"
 #include "tree_ops.hpp"
 
@@ -577,13 +578,7 @@ static hipError_t launch_xor_parts(const uint32_t* parts, uint64_t nparts, uint3
     return hipGetLastError();
 }
 
-static int cu_count_fold() {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    return cus;
-}
+static int cu_count_fold() { return cu_count(); }   // the calling thread's CU budget (dpf_kernels.hip)
 
 constexpr uint64_t kFoldMaxBlocks = 1024;          // workgroups per launch (partials area)
 constexpr uint64_t kFoldPartBytes = 64 * 4 * 32 * 2;   // largest part: 64*KW keys x 32C bytes, KW*C <= 8

@@ -103,6 +103,8 @@ SIGNATURES = {
     "dpf_pir_db_create": (_int, [_u8p, _u64, _u32, _int, ctypes.POINTER(_vp)]),
     "dpf_pir_answer": (_int, [_vp, _u8p, _sz, _sz, _u8p]),
     "dpf_pir_db_free": (None, [_vp]),
+    "dpf_stream_create_cu_masked": (_int, [_int, _u32, _u32, ctypes.POINTER(_vp)]),
+    "dpf_stream_destroy": (_int, [_vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -456,6 +458,21 @@ def aes_mmo_dev(d_in, d_out, nblocks: int, impl: int = AES_TTABLE, right: bool =
     """aes128MMO iterated `reps` times over nblocks HBM blocks (both back ends)."""
     _check(lib().dpf_aes_mmo_dev(device, impl, 1 if right else 0, _ptr(d_in), _ptr(d_out), nblocks, reps,
                                  _stream_handle(stream)))
+
+
+# ------------------------------------------------- CU-partitioned streams ---
+def stream_create_cu_masked(cu_first: int, cu_count: int, device: int = 0):
+    """A torch stream (ExternalStream) whose kernels run only on CUs
+    [cu_first, cu_first + cu_count) of `device`; the _dev entry points size
+    their grids to those CUs.  Release with stream_destroy()."""
+    import torch
+    h = _vp()
+    _check(lib().dpf_stream_create_cu_masked(device, cu_first, cu_count, ctypes.byref(h)))
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", device))
+
+
+def stream_destroy(stream) -> None:
+    _check(lib().dpf_stream_destroy(_stream_handle(stream)))
 
 
 # ------------------------------------------------------- streaming fold ---

@@ -143,6 +143,17 @@ int dpf_eval_batch_dev(int device, const uint8_t* d_keys, size_t key_len, size_t
                        size_t pts_per_key, uint32_t logN, uint8_t* d_out, void* d_work, size_t work_bytes,
                        void* stream);
 
+/* ---- CU-partitioned streams (no reference counterpart: engine plumbing) -
+ * A stream whose kernels may run only on CUs [cu_first, cu_first+cu_count)
+ * of `device` (hipExtStreamCreateWithCUMask).  Bit i of the mask is spread
+ * across the XCDs (consecutive bits land on different XCDs), so any
+ * contiguous range is balanced over the chip.  The _dev entry points size
+ * their grids to the stream's CUs.  Two such streams over disjoint ranges let
+ * an LDS-bound kernel (the tree) and an HBM-bound one (the PIR fold) run side
+ * by side without sharing a CU.  Destroy with dpf_stream_destroy. */
+int dpf_stream_create_cu_masked(int device, uint32_t cu_first, uint32_t cu_count, void** stream);
+int dpf_stream_destroy(void* stream);
+
 /* ---- AES back end of the tree kernels (BASELINE configs[1]) ------------
  * DPF_AES_TTABLE: T-tables staged in LDS (aes_ttable.hpp).
  * DPF_AES_BITSLICED: table-free byte-sliced AES, 8 blocks per lane in VALU
