@@ -504,12 +504,38 @@ def reference_shapes_gpu(c: Ctx) -> dict:
         for _ in range(reps):
             dpf.EvalFull(key, logN)
         api_ms = (time.perf_counter() - t0) / reps * 1e3
+        # The C ABI itself, as a cgo caller binds it (dpf_evalfull, no Python
+        # buffer handling): into one reused host buffer, and into a fresh
+        # np.empty per call (first touch of its pages inside the call, like a
+        # fresh Go slice, dpf.go:251).  Medians.
+        L, kk, nbytes = dpf.lib(), np.frombuffer(key, np.uint8), dpf.evalfull_len(logN)
+        reused = np.empty(nbytes, np.uint8)
+
+        def capi(buf):
+            rc = L.dpf_evalfull(dpf._buf(kk), kk.size, logN, dpf._buf(buf))
+            assert rc == 0, rc
+
+        def med_ms(f, n):
+            f()
+            ts = []
+            for _ in range(n):
+                t0 = time.perf_counter()
+                f()
+                ts.append(time.perf_counter() - t0)
+            return float(np.median(ts)) * 1e3
+        capi_reused = med_ms(lambda: capi(reused), 31)
+        capi_fresh = med_ms(lambda: capi(np.empty(nbytes, np.uint8)), 31)
         r = {"logN": logN, "alpha": sh["alpha"], "source": sh["source"],
              "gpu_dev_ms_per_evalfull": round(dev_ms, 4),
              "gpu_api_ms_per_evalfull": round(api_ms, 4),
+             "capi_reused_ms": round(capi_reused, 4), "capi_fresh_ms": round(capi_fresh, 4),
+             "capi_reused_GBps": round(nbytes / (capi_reused * 1e-3) / 1e9, 2),
+             "capi_fresh_GBps": round(nbytes / (capi_fresh * 1e-3) / 1e9, 2),
              "gpu_dev_points_per_s": (1 << logN) / (dev_ms * 1e-3),
              "gpu_note": "dev: dpf_evalfull_batch_dev of one key, output left in HBM; api: dpf.EvalFull "
-                         "(C ABI dpf_evalfull, fresh host output incl. its D2H), mean of %d calls" % reps}
+                         "(C ABI dpf_evalfull into a fresh np.empty, returned as a view, incl. its D2H), mean of "
+                         "%d calls; capi_*: dpf_evalfull called directly (ctypes), medians of 31, output cut into "
+                         ">= 4 subtree slabs so kernel, PCIe copy and host copy overlap" % reps}
         if name == "dpf_main":
             t0 = time.perf_counter()
             k2, _ = dpf.Gen(123, logN)
@@ -659,7 +685,12 @@ def wl_eval(c: Ctx) -> dict:
                   ms_per_step=sec * 1e3, scaling="weak", data="synthetic keys + uniform points",
                   config={"workload": f"batched Eval, {nk} keys x {ppk} points, logN={logN} per GPU "
                                       f"(BASELINE configs[2])", "logN": logN, "parallelism": f"key-shard x{c.world}"},
-                  aes_blocks_per_s=aes * c.world / sec)
+                  aes_blocks_per_s=aes * c.world / sec,
+                  aes_blocks_per_s_executed=aes_done * c.world / sec,
+                  aes_blocks_note=(f"aes_blocks_per_s is reference-equivalent: stop+1 = {stop_of(logN) + 1} AES per "
+                                   f"query (SURVEY 8d A_eval), more than the kernels run; "
+                                   f"aes_blocks_per_s_executed counts the {aes_done / q:.2f} per query they compute "
+                                   f"(shared frontier at level {L} + per-query walks)"))
     line["roofline"] = prg_roofline(aes_done / (k_ms * 1e-3), "k_unpack+[k_evalfull<nodes>]+k_eval", k_ms, 
                                     q * 9 + nk * (stop_of(logN) + 2) * 32, workload="eval")
     if L:

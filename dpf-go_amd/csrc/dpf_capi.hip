@@ -443,6 +443,7 @@ hipError_t tree_from_keys(const uint8_t* d_keys, size_t klen, size_t nk, uint32_
 // i-1 (d.cst, into a pinned slot) and the host copy of chunk i-2 (pinned ->
 // caller buffer, CopyPool) overlap; two device and two pinned slots.
 constexpr size_t kStageBytes = (size_t)32 << 20;
+constexpr size_t kSlabMinOut = (size_t)8 << 20;    // one key's output from which it is cut into >= 4 slabs
 
 int ensure_staging(Dev& d, size_t chunk_cap) {
     if (!d.cst) {
@@ -525,13 +526,18 @@ int full_on_device(Dev& d, const uint8_t* keys, size_t klen, size_t nk, uint32_t
     const uint8_t* dk = (const uint8_t*)d.keys.p;
     uint32_t pb = 0;                                      // one key's output exceeds a chunk: subtree slabs
     while ((olen >> pb) > kStageBytes) ++pb;
+    // A key whose output is >= kSlabMinOut goes in >= 4 subtree slabs even
+    // when it fits one chunk, so its kernel, PCIe copy and host copy overlap
+    // (BenchmarkEvalFull's logN = 28 is one 32 MiB key: as one chunk, the
+    // three ran back to back).
+    if (olen >= kSlabMinOut && pb < 2) pb = 2;
     // Every chunk straight from the key bytes when each chunk shape allows it
     // (tree_from_keys), else the keys are expanded once for all chunks.
-    const bool raw = !bs && (olen <= kStageBytes ? dpfk::evalfull_raw_ok(std::min(per, nk), stop, 0) &&
+    const bool raw = !bs && (pb == 0 ? dpfk::evalfull_raw_ok(std::min(per, nk), stop, 0) &&
                                                        (nk % per == 0 || dpfk::evalfull_raw_ok(nk % per, stop, 0))
                                                  : dpfk::evalfull_raw_ok(1, stop, pb));
     if (!raw) HIP_TRY(expand_keys(dk, klen, nk, stop, w, d.st, bs));
-    if (olen <= kStageBytes) {
+    if (pb == 0) {
         const size_t nch = (nk + per - 1) / per;
         return pipeline_d2h(d, nch, std::min(per, nk) * olen, [&](size_t i, uint8_t* dbuf, size_t& bytes, size_t& off) {
             const size_t k0 = i * per, n = std::min(per, nk - k0);

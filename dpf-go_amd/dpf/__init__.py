@@ -277,14 +277,22 @@ def _eval_fn():
     return _eval_proto
 
 
-def EvalFull(key: bytes, logN: int) -> bytes:
-    """dpf.go:243 — the share of f_alpha over the whole domain, packed bits."""
+def EvalFull(key: bytes, logN: int, out: Optional[np.ndarray] = None) -> memoryview:
+    """dpf.go:243 — the share of f_alpha over the whole domain, packed bits.
+
+    Returns a writable bytes-like view of a fresh buffer (the Go function
+    returns a fresh []byte, dpf.go:251): dpf_evalfull writes every byte of it
+    once, with no zero fill before and no copy after.  `out` (uint8,
+    evalfull_len(logN) bytes, C-contiguous) reuses a caller buffer instead."""
     if logN > 63:   # the reference panics allocating 2^(logN-3) bytes (dpf.go:251)
         raise DPFPanic(DPF_ERR_PARAM, "dpf: logN > 63")
     kk = _as_u8(key)
-    out = np.zeros(evalfull_len(logN), np.uint8)
+    n = evalfull_len(logN)
+    if out is None:
+        out = np.empty(n, np.uint8)
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size == n
     _check(lib().dpf_evalfull(_buf(kk), kk.size, logN, _buf(out)))
-    return out.tobytes()
+    return out.reshape(-1).data
 
 
 def evalfull_batch(keys: np.ndarray, logN: int, ngpus: int = 0, out: Optional[np.ndarray] = None) -> np.ndarray:
