@@ -565,7 +565,7 @@ static hipError_t launch_xor_parts(const uint32_t* parts, uint64_t nparts, uint3
     // Part slices per answer word, one atomic each: 16 for <= 256 partials
     // (the PIR rank at N = 8: step 0.0733-0.0737 vs 0.0740-0.0745 ms with 64,
     // 8 in between), 64 above (one GPU, 768 partials: 0.3799-0.3802 vs
-    // 0.3811-0.3817 with 16); tools/r05_xys.sh, profiles/r05/xor_parts/.
+    // 0.3811-0.3817 with 16); tools/archive/r05_xys.sh, profiles/r05/xor_parts/.
     // DPF_XOR_PARTS_YS=<n> (measurement only) fixes it.
     static const uint64_t yenv = [] {
         const char* e = getenv("DPF_XOR_PARTS_YS");
@@ -1334,7 +1334,7 @@ static int fold_glds_mode() {
 #endif
 
 // The DB pieces of a matrix-core fold over at least this many DB bytes are
-// loaded nontemporal.  r05 (tools/r05_nt.sh, profiles/r05/fold_nt/, B = 64,
+// loaded nontemporal.  r05 (tools/archive/r05_nt.sh, profiles/r05/fold_nt/, B = 64,
 // fold us, nontemporal vs default): 2^24 x 32 B (512 MiB, twice the chip's
 // last-level cache) 123-125 vs 135-138, and B = 16 95 vs 105-107; 2^23 66-69
 // vs 67-74; but 2^22 39-40 vs 35-36 and 2^21 (an N = 8 rank) 25.5 vs 24.7:
@@ -1377,14 +1377,14 @@ hipError_t launch_mfma_mt(const uint32_t* bits, uint64_t wpk, const uint8_t* dbs
     const bool ntdb = nsg * 256 * 32 >= fold_nt_min_bytes();
     // Two workgroups per CU instead of the occupancy limit (3 at 33-64 keys)
     // for cached DB slices and for the one-key-tile shape: fewer partials to
-    // combine and less per-workgroup overhead (r05, tools/r05_fpercu.sh,
+    // combine and less per-workgroup overhead (r05, tools/archive/r05_fpercu.sh,
     // profiles/r05/fold_blocks/, medians of 5: 2^21 x 32 B 22.6 vs 24.7 us,
     // 2^22 34.8 vs 36.0, B = 16 at 2^24 91.9 vs 96.6, B = 32 96.3 vs 99.8;
     // but B = 64 at 2^23 / 2^24 67.9 / 130.7 vs 67.0 / 125.9).  One per CU
     // for 33-64 keys over a slice of <= 64 MiB (the PIR rank at N = 8): rank
     // step 0.0741-0.0750 vs 0.0742-0.0759 ms, lower in 5 of 6 interleaved
     // pairs; at N = 4 (128 MiB) the pairs split 3 / 3 and the fold alone was
-    // slower (37.6 vs 33.9 us), so it keeps 2 (tools/r05_fpercu1.sh,
+    // slower (37.6 vs 33.9 us), so it keeps 2 (tools/archive/r05_fpercu1.sh,
     // profiles/r05/fold_blocks/per_cu1_*.txt).
     const bool small_slice = nsg * 256 * 32 <= (64ull << 20);
     uint64_t pcu = small_slice && MT == 2 ? 1 : (!ntdb || MT == 1) && per_cu > 2 ? 2 : (uint64_t)per_cu;

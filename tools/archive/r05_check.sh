@@ -12,4 +12,4 @@ rc=$?; tail -3 "$OUT/tests.log"; grep -E "PASSED|FAILED|SKIPPED" "$OUT/tests.log
 DPF_LIB=dpf-go_amd/lib/variants/libdpf_hip_exp.so timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
    tests/test_gpu_pir_fused.py > "$OUT/tests_exp.log" 2>&1 || { tail -20 "$OUT/tests_exp.log"; exit 1; }
 tail -2 "$OUT/tests_exp.log"
-bash tools/r05_pir8.sh r05_pir8
+bash tools/archive/r05_pir8.sh r05_pir8

@@ -1,7 +1,7 @@
 #!/bin/bash
 # r05: k_eval2 with wave-uniform keys (CWs in SGPRs) vs per-lane keys
 # (DPF_EVAL_UNIFORM=0) at configs[2], Eval parity tests on the product and
-# the experimental build, then the fold's PMC passes (tools/r05_pmc_fold.sh).
+# the experimental build, then the fold's PMC passes (tools/archive/r05_pmc_fold.sh).
 set -uo pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$REPO"
@@ -22,4 +22,4 @@ for round in 1 2 3; do
     grep '^{' "$OUT/eval_u${u}_$round.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('uniform=$u round $round', round(d['ms_per_step'],4), 'ms', round(d['value']/1e9,3), 'G q/s kernel', d['roofline']['kernel_ms'])"
   done
 done
-bash tools/r05_pmc_fold.sh r05_pmc_fold64 > "$OUT/pmc64.txt" 2>&1; tail -3 "$OUT/pmc64.txt"
+bash tools/archive/r05_pmc_fold.sh r05_pmc_fold64 > "$OUT/pmc64.txt" 2>&1; tail -3 "$OUT/pmc64.txt"

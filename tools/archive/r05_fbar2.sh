@@ -9,7 +9,7 @@ OUT="gpurun_out/${1:-r05_fbar2}"; mkdir -p "$OUT"
 timeout -k 10 500 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_fold.py \
    tests/test_gpu_per_rank.py tests/test_gpu_pir.py > "$OUT/tests.log" 2>&1 || { tail -30 "$OUT/tests.log"; exit 1; }
 tail -1 "$OUT/tests.log"
-bash tools/r05_fbar.sh "$(basename $OUT)"
+bash tools/archive/r05_fbar.sh "$(basename $OUT)"
 C="--steps 100 --warmup 10 --no-cpu-baseline --no-api --no-variants --no-sweep --no-workloads"
 for r in 1 2 3; do
   for w in 1 8; do

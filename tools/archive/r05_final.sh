@@ -1,12 +1,12 @@
 #!/bin/bash
-# r05 final: the round profile (tools/r05_round.sh) on the final code, then
+# r05 final: the round profile (tools/archive/r05_round.sh) on the final code, then
 # the per-rank shares of the strong-scaling splits at N = 4 / 8 (emulated
 # rank 0) for DESIGN.md §7.
 set -uo pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$REPO"
 TAG="${1:-r05_final}"
-bash tools/r05_round.sh "$TAG" || exit 1
+bash tools/archive/r05_round.sh "$TAG" || exit 1
 OUT="gpurun_out/$TAG"
 C="--steps 100 --warmup 10 --no-cpu-baseline --no-api --no-variants --no-sweep --no-workloads"
 for r in 1 2; do

@@ -38,5 +38,5 @@ for r in 1 2; do
     done
   done
 done
-bash tools/r05_depth.sh r05_depth
-bash tools/r05_small.sh r05_small
+bash tools/archive/r05_depth.sh r05_depth
+bash tools/archive/r05_small.sh r05_small

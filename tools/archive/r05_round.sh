@@ -2,7 +2,7 @@
 # r05 round profile: the GPU parity suite, smoke(), the driver's default bench
 # command, a rocprofv3 kernel trace of it, and FETCH_SIZE / WRITE_SIZE passes
 # (one counter per run) of every workload for roofline.traffic.
-# Usage: tools/r05_round.sh <tag>.  Each GPU step has its own time limit;
+# Usage: tools/archive/r05_round.sh <tag>.  Each GPU step has its own time limit;
 # the first failure ends the call.
 set -uo pipefail
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
