@@ -125,3 +125,52 @@ def test_workspace_reexpanded_by_another_entry_point_is_not_stale():
         assert e.value.code == dpf.DPF_ERR_PARAM
     finally:
         dpf.set_aes_impl(prev)
+
+
+def test_cu_masked_streams_give_identical_results():
+    """dpf_stream_create_cu_masked: kernels on a stream limited to a CU range
+    (grids sized to it) give the same bytes as on the whole device; the
+    tree and the PIR fold on two disjoint ranges at once agree with the
+    oracle; bad ranges are refused."""
+    import torch
+    dev = torch.device("cuda", 0)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    with pytest.raises(dpf.DPFPanic) as e:
+        dpf.stream_create_cu_masked(0, 0)
+    assert e.value.code == dpf.DPF_ERR_PARAM
+    with pytest.raises(dpf.DPFPanic) as e:
+        dpf.stream_create_cu_masked(ncu - 4, 8)
+    assert e.value.code == dpf.DPF_ERR_PARAM
+    T = dpf.stream_create_cu_masked(16, ncu - 16)
+    F = dpf.stream_create_cu_masked(0, 16)
+    try:
+        logN, nk = 18, 48
+        al, s0, s1 = synth.key_seeds(nk, logN, first=515)
+        ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+        kl, ol = dpf.key_len(logN), dpf.evalfull_len(logN)
+        d_keys = torch.from_numpy(ka.reshape(-1)).to(dev)
+        d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=dev)
+        bits = torch.full((nk * ol,), 0x5A, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        dpf.evalfull_batch_dev(d_keys, kl, nk, logN, bits, d_work, stream=T)
+        T.synchronize()
+        want = oracle.evalfull_batch(ka, logN, nthreads=8)
+        assert np.array_equal(bits.cpu().numpy().reshape(nk, ol), want)
+        nrec = (1 << logN) - 300
+        db = synth.db_bytes(nrec * 32).reshape(nrec, 32)
+        d_dbs = torch.empty(dpf.pir_db_sliced_size(nrec), dtype=torch.uint8, device=dev)
+        dpf.pir_db_slice_dev(torch.from_numpy(db.reshape(-1)).to(dev), nrec, d_dbs, stream=F)
+        d_ans = torch.empty(nk * 32, dtype=torch.uint8, device=dev)
+        fwork = torch.empty(dpf.xor_fold_workspace_size(), dtype=torch.uint8, device=dev)
+        bits2 = torch.empty_like(bits)
+        # fold the first bits on F while T evaluates the same keys again
+        dpf.xor_fold_sliced_dev(bits, ol, nk, d_dbs, nrec, d_ans, fwork, stream=F)
+        dpf.evalfull_batch_dev(d_keys, kl, nk, logN, bits2, d_work, stream=T)
+        torch.cuda.synchronize()
+        assert torch.equal(bits, bits2)
+        want_ans = oracle.pir_answer_batch(ka, logN, db, nrec, nslices=1, nthreads=8)[:, 0, :]
+        assert np.array_equal(d_ans.cpu().numpy().reshape(nk, 32), want_ans)
+    finally:
+        torch.cuda.synchronize()
+        dpf.stream_destroy(T)
+        dpf.stream_destroy(F)
