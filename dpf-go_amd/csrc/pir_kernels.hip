@@ -806,8 +806,11 @@ constexpr int kE8M0One = 127;       // block scale 2^0
 // the kernel moved the large-tile accumulators out of AGPRs and spilled them:
 // 2.5x slower at 256 keys, r05.)  wlim: selection words per key row from
 // `bits` (the row stride stays wpk), so a pass can start mid-row.
+#ifndef DPF_FOLD_MINB4
+#define DPF_FOLD_MINB4 2   // min workgroups per CU the <=4-tile shapes are compiled for (A/B: 4 = <=128 VGPRs)
+#endif
 template <int MT, int NT, int SG, int KG, int SGM = 0, bool NTDB = false>
-__global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? 2 : 1) void k_fold_mfma(
+__global__ __launch_bounds__(64 * (8 / NT) * KG, (MT * NT <= 4) ? DPF_FOLD_MINB4 : 1) void k_fold_mfma(
     const uint32_t* __restrict__ bits, uint64_t wpk, const uint4* __restrict__ dbs, uint64_t nsg, uint32_t nkeys,
     uint64_t sg_per_block, uint32_t* __restrict__ parts, uint32_t* __restrict__ zero, uint64_t zero_words,
     uint64_t wlim, uint32_t sgm_keys = 0) {
@@ -1487,6 +1490,7 @@ hipError_t launch_pir_fold_sliced(const uint32_t* bits, uint64_t words_per_key, 
             if (DPF_FOLD_SHAPE64 == 1) e = DPF_MT(2, 2, 4, 1);
             else if (DPF_FOLD_SHAPE64 == 2) e = DPF_MT(1, 2, 4, 2);
             else if (DPF_FOLD_SHAPE64 == 3) e = DPF_MT(2, 4, 2, 1);
+            else if (DPF_FOLD_SHAPE64 == 4) e = DPF_MT(2, 2, 1, 1);
             else e = DPF_MT(2, 2, 2, 1);
         } else if (nk <= 128) {
             if (DPF_FOLD_SHAPE == 1) e = DPF_MT(2, 4, 2, 2);

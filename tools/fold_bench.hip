@@ -15,6 +15,17 @@
 #endif
 #include FOLD_SRC
 
+// pir_kernels.hip sizes its grids with dpfk::cu_count() (dpf_kernels.hip in
+// the library): the whole device here.
+namespace dpfk {
+int cu_count() {
+    int d = 0, c = 256;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        c = 256;
+    return c;
+}
+}  // namespace dpfk
+
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
 int main(int argc, char** argv) {
