@@ -24,4 +24,8 @@ done
     -o p --output-format csv -- python3 "$REPO/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-api --no-variants \
     > "$REPO/gpurun_out/$T/pmc_icache.log" 2>&1 ) || echo "icache pass failed (see pmc_icache.log)"
 { command -v go && go version; } > "gpurun_out/$T/go_probe.txt" 2>&1 || echo "go: not found on the GPU box ($(date -u +%FT%TZ))" > "gpurun_out/$T/go_probe.txt"
+# gpurun copies back at most 64 MiB: keep the summaries, drop raw per-dispatch
+# CSVs (counter_collection / kernel_trace rows) once they have been summarised.
+find "gpurun_out/$T" -type f -size +2M -printf '%s %p\n' > "gpurun_out/$T/pruned_files.txt"
+find "gpurun_out/$T" -type f -size +2M -delete
 echo "round profile done"
