@@ -150,7 +150,13 @@ template <bool B = false>
 __device__ __forceinline__ void walk_step2(const uint8_t* tab, uint32_t lo, Node& n0, const CW& cw0, uint32_t bit0,
                                            Node& n1, const CW& cw1, uint32_t bit1) {
     Blk c0, c1;
+#if DPF_EXP_NOSEL
+    // Measurement only (wrong answers): the walk with a wave-uniform key, to
+    // bound what the per-lane key select costs.
+    mmo2<B>(tab, lo, KeyFixed<false>{}, n0.s, c0, KeyFixed<false>{}, n1.s, c1);
+#else
     mmo2<B>(tab, lo, KeySel{bit0 ? 0xffffffffu : 0u}, n0.s, c0, KeySel{bit1 ? 0xffffffffu : 0u}, n1.s, c1);
+#endif
     walk_fix(n0, c0, cw0, bit0);
     walk_fix(n1, c1, cw1, bit1);
 }
