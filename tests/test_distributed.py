@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size 2, CPU) tests of the multi-GPU partition
+"""Multi-process (gloo, world_size 2, 4 and 8, CPU) tests of the multi-GPU partition
 logic in dpf/shard.py: subtree-split EvalFull reassembly and the PIR partial
 answer gather + host XOR fold.  Per-rank compute uses the CPU oracle here
 (test infrastructure); on the GPU box the same logic runs over RCCL."""
@@ -57,22 +57,26 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_split_and_pir():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_split_and_pir(world):
+    """The driver's N = 2/4/8 partitions: prefix-log2(N) subtree slices
+    reassemble to the whole EvalFull, and the N DB-slice partial answers
+    gathered and XORed (shard.gather_xor, the RCCL path's gloo twin) equal the
+    whole-DB answer."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=180) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort()
     assert all(r[1] for r in res), "subtree split reassembly failed"
     assert all(r[2] for r in res), "PIR gather+XOR failed"
-    assert res[0][3] == (0, 2048) and res[1][3] == (2048, 4096)
+    assert [r[3] for r in res] == [(r * 4096 // world, (r + 1) * 4096 // world) for r in range(world)]
 
 
 def test_partition_helpers():
@@ -121,6 +125,27 @@ def test_bench_gpus_flag_spawns_ranks():
     assert p["scaling"] == "strong"
     w = run("--workload", "pir", "--pir-per-gpu", "--no-cpu-baseline")
     assert w["scaling"] == "weak"
+
+
+@pytest.mark.parametrize("workload", ["evalfull", "pir"])
+def test_bench_gpus_8_dry_run(workload):
+    """The driver's 8-GPU command shape (`bench.py --gpus 8`): 8 ranks through
+    the same spawn, barriers and max-over-ranks reduction; rank 0 prints one
+    line with n_gpus 8 and the workload's scaling label."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--dry-run", "--workload",
+                        workload, "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.3", "--no-cpu-baseline"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["local_ranks"] == "8" and d["workload"] == workload
+    assert d["scaling"] == ("weak" if workload == "evalfull" else "strong")
 
 
 def test_xor_rows_matches_numpy():
