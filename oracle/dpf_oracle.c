@@ -11,6 +11,10 @@
  * pinned by (a) the FIPS-197 AES-128 known answer, (b) fixed-key KATs
  * computed with OpenSSL (tests/golden/aes_kat.json, script committed), and
  * (c) the reference's own property tests (dpf/dpf_test.go:32-73) restated.
+ * The reference holds no DPF golden vectors and its Gen draws from
+ * crypto/rand (dpf/dpf.go:80-81), so above the AES layer (key layout, CW
+ * arithmetic, leaf order) this oracle is PARITY UNPINNED: the properties in
+ * (c) are all that ties it to the reference.
  *
  * Each function cites the reference line it follows.  Two AES back ends:
  *   - portable: S-box derived from GF(2^8) inversion + affine map (FIPS-197
