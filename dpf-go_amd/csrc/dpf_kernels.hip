@@ -79,6 +79,7 @@ struct Ctx {
     uint8_t* nt;        // node mode: t cursor
     uint32_t groups;    // 4-leaf groups finished (wave priority steps, prio_step)
     const uint32_t* cwl;   // the key's CWs staged in LDS (8 words per level), or nullptr
+    bool sync = false;     // workgroup-uniform: every thread runs the same DFS (DPF_TREE_SYNC barriers)
 };
 
 // Level lvl's correction word for the expansion: from the LDS copy when the
@@ -110,6 +111,9 @@ __device__ __forceinline__ CW ctx_cw(const Ctx& c, uint32_t lvl) {
 //   scaling ranks) step at 1/2, 3/4, 7/8 (DPF_PRIO_STEPS_SMALL 2): at the
 //   PIR shape waves are busy 0.945-0.949 of the span instead of 0.914-0.922
 //   and the span is 244 vs 250-256 us (profiles/r04/prio/).
+#ifndef DPF_TREE_SYNC
+#define DPF_TREE_SYNC 0
+#endif
 #ifndef DPF_PRIO_STEPS_SMALL
 #define DPF_PRIO_STEPS_SMALL 2
 #endif
@@ -129,6 +133,11 @@ __device__ __forceinline__ void prio_step(Ctx& c) {
     else if (x >= t1 * total) __builtin_amdgcn_s_setprio(2);
 #else
     (void)c;
+#endif
+#if DPF_TREE_SYNC
+    // Measurement: a workgroup barrier every DPF_TREE_SYNC groups keeps the
+    // workgroup's waves within one period of each other.
+    if (c.sync && (c.groups % DPF_TREE_SYNC) == 0) __syncthreads();
 #endif
 }
 
@@ -376,6 +385,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     };
     c.groups = 0;
     c.cwl = DPF_DFS_CW_LDS && cw_lds ? s_cw : nullptr;
+    c.sync = DPF_TREE_SYNC && UNIFORM && !NODES && (uint64_t)(blockIdx.x + 1) * Bw <= nunits;
 #if DPF_PRIO_STEPS
     __builtin_amdgcn_s_setprio(3);
 #endif
