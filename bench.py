@@ -120,7 +120,7 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
         r["traffic_note"] = "no PMC profile at this per-rank shape (1/N of the 1-GPU split); traffic not reported"
         return r
     if workload != "evalfull":
-        for rnd in ("r05", "r04", "r03", "r02"):
+        for rnd in ("r06", "r05", "r04", "r03", "r02"):
             name = f"{rnd}_traffic_{workload}.json"
             try:
                 with open(os.path.join(ROOT, "profiles", name)) as f:
@@ -137,7 +137,7 @@ def prg_roofline(aes_rate: float, kernel: str, k_ms: float, hbm_bytes: float, ae
             r["traffic_source"] = f"profiles/{name} (sum of {', '.join(ks)})"
             break
         return r
-    for name in ("r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01_traffic.json"):
+    for name in ("r06_traffic.json", "r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json", "r01_traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 t = json.load(f)
@@ -902,7 +902,7 @@ def pir_breakdown(c: Ctx, W: int, d_db, lo: int, hi: int, nk: int, steps: int) -
     # this exact shape (1 GPU, 64 keys, the fold this run uses).
     traffic, tsrc = None, None
     if W == 1 and nk == 64:
-        for rnd in ("r05", "r04", "r03"):
+        for rnd in ("r06", "r05", "r04", "r03"):
             name = f"{rnd}_traffic_pir.json"
             try:
                 with open(os.path.join(ROOT, "profiles", name)) as f:
