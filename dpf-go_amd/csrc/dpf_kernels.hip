@@ -80,6 +80,8 @@ struct Ctx {
     uint32_t groups;    // 4-leaf groups finished (wave priority steps, prio_step)
     const uint32_t* cwl;   // the key's CWs staged in LDS (8 words per level), or nullptr
     bool sync = false;     // workgroup-uniform: every thread runs the same DFS (DPF_TREE_SYNC barriers)
+    uint32_t* prog = nullptr;   // DPF_PRIO_FEEDBACK: this SIMD's 16 wave-progress slots in LDS
+    uint32_t pslot = 0;         // ... and this wave's slot (hardware wave id)
 };
 
 // Level lvl's correction word for the expansion: from the LDS copy when the
@@ -114,11 +116,33 @@ __device__ __forceinline__ CW ctx_cw(const Ctx& c, uint32_t lvl) {
 #ifndef DPF_TREE_SYNC
 #define DPF_TREE_SYNC 0
 #endif
+#ifndef DPF_PRIO_FEEDBACK
+#define DPF_PRIO_FEEDBACK 3   // priority from the wave's lead over the slowest wave of its SIMD; 0: static steps
+#endif
 #ifndef DPF_PRIO_STEPS_SMALL
 #define DPF_PRIO_STEPS_SMALL 2
 #endif
 template <int DMAX>
 __device__ __forceinline__ void prio_step(Ctx& c) {
+#if DPF_PRIO_FEEDBACK
+    // Feedback form: each wave publishes its finished groups in its SIMD's
+    // LDS slots and reads the others'; the further it leads the slowest wave
+    // of the SIMD (in this workgroup), the lower its issue priority.
+    if (c.prog != nullptr) {
+        const uint32_t d = ++c.groups;
+        c.prog[c.pslot] = d;
+        const uint4* q = reinterpret_cast<const uint4*>(c.prog);
+        const uint4 a = q[0], b = q[1], e = q[2], f = q[3];
+        uint32_t m = min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
+        m = min(m, min(min(min(e.x, e.y), min(e.z, e.w)), min(min(f.x, f.y), min(f.z, f.w))));
+        const uint32_t lead = d - __builtin_amdgcn_readfirstlane(m < d ? m : d);
+        if (lead == 0) __builtin_amdgcn_s_setprio(3);
+        else if (lead == 1) __builtin_amdgcn_s_setprio(2);
+        else if (lead <= DPF_PRIO_FEEDBACK) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+        return;
+    }
+#endif
 #if DPF_PRIO_STEPS
     constexpr int S = DMAX <= 5 ? DPF_PRIO_STEPS_SMALL : DPF_PRIO_STEPS;
     constexpr uint32_t total = DMAX >= 2 ? 1u << (DMAX - 2) : 1u;   // 4-leaf groups per thread
@@ -330,7 +354,7 @@ __global__ void k_unpack(const uint8_t* __restrict__ keys, uint64_t key_len, uin
 // NODES: the same walk, but the 2^D nodes at level ltop + D are written to
 // (uint4*)out / out_t at [key*out_stride + (u mod 2^units_log) * 2^D].
 template <int D, bool UNIFORM, bool NODES, bool RAW = false>
-__global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint32_t* __restrict__ ekeys, uint32_t stop,
+__global__ __launch_bounds__(kTreeBlockMax, kTreeWaves) void k_evalfull(const uint32_t* __restrict__ ekeys, uint32_t stop,
                                                         uint64_t nunits, uint32_t units_log, uint32_t ltop,
                                                         uint64_t sub_base, uint8_t* __restrict__ out,
                                                         uint8_t* __restrict__ out_t, uint64_t out_stride,
@@ -340,7 +364,7 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     const uint64_t t_start = wall_clock64();
 #endif
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kTreeBlock
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // blockDim: 64..kTreeBlockMax
     uint64_t key = u >> units_log;
     if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
     const uint64_t local = u & ((1ull << units_log) - 1);
@@ -367,6 +391,10 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     const bool cw_mine = cw_lds && threadIdx.x < (DPF_DFS_CW_LDS ? stop : ltop);
     CW cw_pre{};
     if (cw_mine) cw_pre = key_cw<RAW>(c.ks, threadIdx.x);   // per-lane level: vector loads
+#if DPF_PRIO_FEEDBACK
+    __shared__ __attribute__((aligned(16))) uint32_t s_prog[64];
+    if (threadIdx.x < 64) s_prog[threadIdx.x] = 0xffffffffu;
+#endif
     fill_table_nobar(s_tab);
     if (cw_mine) {
         *reinterpret_cast<uint4*>(s_cw + 8 * threadIdx.x) = make_uint4(cw_pre.s.c0, cw_pre.s.c1, cw_pre.s.c2, cw_pre.s.c3);
@@ -386,6 +414,17 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     c.groups = 0;
     c.cwl = DPF_DFS_CW_LDS && cw_lds ? s_cw : nullptr;
     c.sync = DPF_TREE_SYNC && UNIFORM && !NODES && (uint64_t)(blockIdx.x + 1) * Bw <= nunits;
+#if DPF_PRIO_FEEDBACK
+    // Only where the workgroup holds all 16 waves of its CU (one
+    // kTreeBlockBig-thread workgroup per CU): with two workgroups per CU a
+    // wave sees half of its SIMD's waves, and steering by them was 3% slower.
+    if (UNIFORM && !NODES && D >= (int)kBigMinD && Bw == 1024u) {
+        const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);   // HW_ID: wave id [3:0], SIMD [5:4]
+        c.prog = s_prog + 16 * ((hw >> 4) & 3u);
+        c.pslot = hw & 15u;
+        c.prog[c.pslot] = 0;
+    }
+#endif
 #if DPF_PRIO_STEPS
     __builtin_amdgcn_s_setprio(3);
 #endif
@@ -423,11 +462,11 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
         // 51 us PIR-rank launch at N = 8).  Node j of step s sits in slot j
         // (left child 2j, right 2j + 1), so after the last step slot i is
         // thread i's subtree root.
-        constexpr uint32_t kFs = DPF_COOP_BFS ? kTreeBlock : (1u << (DPF_QUAD_FAN > 6 ? DPF_QUAD_FAN : 6));
+        constexpr uint32_t kFs = DPF_COOP_BFS ? kTreeBlockMax : (1u << (DPF_QUAD_FAN > 6 ? DPF_QUAD_FAN : 6));
         __shared__ uint32_t s_front[5 * kFs];   // SoA: word k of node j at k * kFs + j
         const uint32_t B = blockDim.x;
         const uint32_t W = 31u - (uint32_t)__builtin_clz(B);
-        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W && B <= (uint32_t)kTreeBlock &&
+        if (DPF_COOP_WALK && (B & (B - 1)) == 0 && W >= 7 && units_log >= W && B <= (uint32_t)kTreeBlockMax &&
             (cw_lds || !DPF_WALK_CW_LDS)) {   // uniform
             // Paths of the shared walk: 2^F, F = 6, or DPF_QUAD_FAN with the
             // quad form when the workgroup has the 4 * 2^F lanes for it.
@@ -509,6 +548,9 @@ __global__ __launch_bounds__(kTreeBlock, kTreeWaves) void k_evalfull(const uint3
     // stores for A/B runs.
     constexpr bool kPair = DPF_PAIR_STORES && UNIFORM && !NODES && D >= 3;
     dfs<D, D, NODES, kPair, UNIFORM, RAW>(c, ltop, n);
+#if DPF_PRIO_FEEDBACK
+    if (c.prog != nullptr) c.prog[c.pslot] = 0xffffffffu;   // done: no longer the slowest
+#endif
 #ifdef DPF_WAVE_TIMES
     // Measurement build only (tools/wave_times.hip): per wave, start / end
     // (wall clock) and the hardware ids of the CU it ran on.
@@ -1209,9 +1251,12 @@ static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes, uint32_t 
     }();
     const uint32_t dmax = span < kMaxD ? span : kMaxD;
     auto threads = [&](uint32_t dd) { return span - dd >= 40 ? ~0ull : nkeys << (span - dd); };
+    auto block = [&](uint32_t dd) {
+        return pick_block(threads(dd), !nodes && dd >= kBigMinD ? (uint32_t)kTreeBlockBig : (uint32_t)kTreeBlock);
+    };
     if (forced >= 0) {
         const uint32_t d = dmax < (uint32_t)forced ? dmax : (uint32_t)forced;
-        return {d, pick_block(threads(d), kTreeBlock)};
+        return {d, block(d)};
     }
     constexpr double kLat = 1.9e-6;       // one AES-MMO of a thread on a lightly loaded CU
     constexpr double kPerWave = 0.2e-6;   // ... per resident wave when the CU's LDS pipe is shared
@@ -1228,7 +1273,7 @@ static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes, uint32_t 
         // The shared workgroup walk (k_evalfull, DPF_COOP_WALK): one wave walks
         // the top ltop - W + 6 levels alone (latency, once per round of
         // workgroups), every thread the last W - 6.
-        const uint32_t bl = pick_block(threads(d), kTreeBlock);
+        const uint32_t bl = block(d);
         const uint32_t W = 31u - (uint32_t)__builtin_clz(bl);
         if (DPF_COOP_WALK && span - d >= 6 && (bl & (bl - 1)) == 0 && W >= 7 && span - d >= W) {
             walk = DPF_COOP_BFS ? 0.0 : (double)(W - 6);               // BFS: W - 6 lightly loaded steps instead
@@ -1244,7 +1289,7 @@ static TreeShape pick_shape(uint32_t span, uint64_t nkeys, bool nodes, uint32_t 
             best = d;
         }
     }
-    return {best, pick_block(threads(best), kTreeBlock)};
+    return {best, block(best)};
 }
 
 // Tree pass over every key: leaves of the subtree (prefix_bits, prefix) when

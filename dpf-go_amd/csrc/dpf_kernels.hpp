@@ -12,9 +12,19 @@ constexpr int kBlock = 512;    // threads per workgroup (8 waves); 2 workgroups 
 #ifndef DPF_TREE_WAVES
 #define DPF_TREE_WAVES 4
 #endif
+#ifndef DPF_TREE_BLOCK_BIG
+#define DPF_TREE_BLOCK_BIG 1024
+#endif
 // Tree kernel geometry: 2 workgroups of kTreeBlock threads per CU (LDS-bound),
-// kTreeWaves waves per SIMD (VGPR budget).  Build-time knobs for A/B runs.
+// kTreeWaves waves per SIMD (VGPR budget).  Leaf launches with deep
+// per-thread subtrees (D >= kBigMinD: configs[1], configs[3]) use one
+// kTreeBlockBig-thread workgroup per CU instead, so that all 16 waves of a CU
+// share one LDS and can balance their progress (prio_step feedback form).
+// Build-time knobs for A/B runs.
 constexpr int kTreeBlock = DPF_TREE_BLOCK;
+constexpr int kTreeBlockBig = DPF_TREE_BLOCK_BIG;
+constexpr int kTreeBlockMax = kTreeBlock > kTreeBlockBig ? kTreeBlock : kTreeBlockBig;
+constexpr uint32_t kBigMinD = 6;
 constexpr int kTreeWaves = DPF_TREE_WAVES;
 constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
 constexpr uint32_t kMaxFrontierHbm = 16;  // batched Eval, HBM frontier: deepest shared level
