@@ -720,6 +720,9 @@ __device__ __forceinline__ void eval_pair_walk(const uint32_t* __restrict__ ekey
 #ifndef DPF_EVAL_PERSIST
 #define DPF_EVAL_PERSIST 1   // k_eval_persist for frontier Eval with wave-uniform keys (env DPF_EVAL_PERSIST=0: k_eval2)
 #endif
+#ifndef DPF_EVAL_FEEDBACK
+#define DPF_EVAL_FEEDBACK 3   // k_eval_persist: priority from the wave's lead over its SIMD's slowest; 0: fixed steps
+#endif
 #ifndef DPF_EVAL_CW_LDS
 #define DPF_EVAL_CW_LDS 1   // k_eval_persist: each pair's key records staged in LDS by LDS-DMA (A/B: 0)
 #endif
@@ -905,10 +908,21 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
         return p;
     };
     if (iters == 0) return;                               // uniform over the grid
+#if DPF_EVAL_FEEDBACK
+    // Wave-progress slots per SIMD, as the tree kernel's prio_step feedback form.
+    __shared__ __attribute__((aligned(16))) uint32_t s_prog[64];
+    if (threadIdx.x < 64) s_prog[threadIdx.x] = 0xffffffffu;
+#endif
     issue_x(0, 0);
     if (iters > 1) issue_x(1, 1);
     fill_table(s_tab);
     __builtin_amdgcn_s_setprio(3);
+#if DPF_EVAL_FEEDBACK
+    const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);
+    uint32_t* prog = s_prog + 16 * ((hw >> 4) & 3u);
+    const uint32_t pslot = hw & 15u;
+    prog[pslot] = 0;
+#endif
     issue_nodes(0, 0);
     PairIn p = read_pair(0);
     if (iters > 1) issue_nodes(1, 1);
@@ -917,9 +931,25 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
         issue_x(2, 0);
     }
     for (uint64_t it = 0; it < iters; ++it) {
+#if DPF_EVAL_FEEDBACK
+        if ((it & 3) == 0) {
+            const uint32_t d = (uint32_t)it;
+            prog[pslot] = d;
+            const uint4* q = reinterpret_cast<const uint4*>(prog);
+            const uint4 a = q[0], b = q[1], e = q[2], f = q[3];
+            uint32_t m = min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
+            m = min(m, min(min(min(e.x, e.y), min(e.z, e.w)), min(min(f.x, f.y), min(f.z, f.w))));
+            const uint32_t lead = d - __builtin_amdgcn_readfirstlane(m < d ? m : d);
+            if (lead == 0) __builtin_amdgcn_s_setprio(3);
+            else if (lead <= 4) __builtin_amdgcn_s_setprio(2);
+            else if (lead <= 4 * DPF_EVAL_FEEDBACK) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#else
         if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
         else if (it * 16 >= 12 * iters) __builtin_amdgcn_s_setprio(2);
+#endif
         const uint64_t pr = it * nthr + gt;
 #if DPF_EVAL_CW_LDS
         const uint32_t* cwp = cw_slots ? &sl.cw[it & 1][0] : nullptr;
@@ -942,6 +972,9 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
             issue_x(it + 3, (int)((it + 1) & 1));
         }
     }
+#if DPF_EVAL_FEEDBACK
+    prog[pslot] = 0xffffffffu;
+#endif
 }
 
 #ifndef DPF_EVAL_TRIE_KERNEL
