@@ -24,7 +24,10 @@ constexpr int kBlock = 512;    // threads per workgroup (8 waves); 2 workgroups 
 constexpr int kTreeBlock = DPF_TREE_BLOCK;
 constexpr int kTreeBlockBig = DPF_TREE_BLOCK_BIG;
 constexpr int kTreeBlockMax = kTreeBlock > kTreeBlockBig ? kTreeBlock : kTreeBlockBig;
-constexpr uint32_t kBigMinD = 6;
+#ifndef DPF_BIG_MIN_D
+#define DPF_BIG_MIN_D 6
+#endif
+constexpr uint32_t kBigMinD = DPF_BIG_MIN_D;
 constexpr int kTreeWaves = DPF_TREE_WAVES;
 constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
 constexpr uint32_t kMaxFrontierHbm = 16;  // batched Eval, HBM frontier: deepest shared level
