@@ -437,11 +437,14 @@ def wl_evalfull(c: Ctx) -> dict:
                                   "points_per_s": nk * (1 << logN) / (t2 / max(5, a.steps // 2)),
                                   "bit_identical_first_64_keys": bool(torch.equal(ref, d_out.view(nk, olen)[:64]))}
     pipelined = None
-    if c.world == 1 and not a.no_variants and not a.strong:
+    if c.world == 1 and a.pipelined and not a.strong:
         # A server with a queue of batches: consecutive batches on two streams
         # (own output and workspace each), so the last waves of one launch
         # overlap the first of the next.  Reported beside `value`, which stays
-        # the one-stream step that the kernel roofline describes.
+        # the one-stream step that the kernel roofline describes.  Opt-in
+        # (--pipelined): overlapped launches last longer each, so in the
+        # default run they would skew a kernel trace's average for the
+        # headline kernel away from the line's roofline.kernel_ms.
         d_out2 = torch.empty_like(d_out)
         d_work2 = torch.empty_like(d_work)
         sts = [c.stream, torch.cuda.Stream(c.dev)]
@@ -1137,6 +1140,8 @@ def main() -> None:
     ap.add_argument("--aes", choices=["ttable", "bitsliced"], default=None,
                     help="tree-kernel AES back end for the headline (default: the library's)")
     ap.add_argument("--no-variants", action="store_true", help="skip timing the other AES back end")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="evalfull: also time batches alternating over two streams (reported as 'pipelined')")
     ap.add_argument("--no-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) API rates")
     ap.add_argument("--no-sweep", action="store_true", help="pir: skip the B in {1,16,64,256} batch sweep")
     ap.add_argument("--strong", action="store_true",
