@@ -122,24 +122,38 @@ __device__ __forceinline__ CW ctx_cw(const Ctx& c, uint32_t lvl) {
 #ifndef DPF_PRIO_STEPS_SMALL
 #define DPF_PRIO_STEPS_SMALL 2
 #endif
+// Progress feedback (r06).  A kernel that runs one 1024-thread workgroup per
+// CU keeps 16 LDS slots per SIMD (indexed by the hardware wave id, HW_ID
+// bits [3:0]; SIMD in bits [5:4]; ~0 = empty or finished).  A wave stores its
+// progress d in its slot, reads its SIMD's 16 slots and sets its issue
+// priority by its lead over the slowest of them: 3 when it is the slowest,
+// 2 within `near`, 1 within `far`, else 0.  Fixed thresholds (below) cannot
+// tell a wave that is ahead from one whose SIMD is simply fast.
+__device__ __forceinline__ uint32_t* prog_slots(uint32_t* s_prog, uint32_t& slot) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);   // HW_ID
+    slot = hw & 15u;
+    return s_prog + 16 * ((hw >> 4) & 3u);
+}
+__device__ __forceinline__ void prio_by_lead(uint32_t* slots, uint32_t slot, uint32_t d, uint32_t near,
+                                             uint32_t far) {
+    slots[slot] = d;
+    const uint4* q = reinterpret_cast<const uint4*>(slots);
+    const uint4 a = q[0], b = q[1], e = q[2], f = q[3];
+    uint32_t m = min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
+    m = min(m, min(min(min(e.x, e.y), min(e.z, e.w)), min(min(f.x, f.y), min(f.z, f.w))));
+    const uint32_t lead = d - __builtin_amdgcn_readfirstlane(m < d ? m : d);
+    if (lead == 0) __builtin_amdgcn_s_setprio(3);
+    else if (lead <= near) __builtin_amdgcn_s_setprio(2);
+    else if (lead <= far) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
 template <int DMAX>
 __device__ __forceinline__ void prio_step(Ctx& c) {
 #if DPF_PRIO_FEEDBACK
-    // Feedback form: each wave publishes its finished groups in its SIMD's
-    // LDS slots and reads the others'; the further it leads the slowest wave
-    // of the SIMD (in this workgroup), the lower its issue priority.
+    // Feedback form (progress = finished 4-leaf groups).
     if (c.prog != nullptr) {
-        const uint32_t d = ++c.groups;
-        c.prog[c.pslot] = d;
-        const uint4* q = reinterpret_cast<const uint4*>(c.prog);
-        const uint4 a = q[0], b = q[1], e = q[2], f = q[3];
-        uint32_t m = min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
-        m = min(m, min(min(min(e.x, e.y), min(e.z, e.w)), min(min(f.x, f.y), min(f.z, f.w))));
-        const uint32_t lead = d - __builtin_amdgcn_readfirstlane(m < d ? m : d);
-        if (lead == 0) __builtin_amdgcn_s_setprio(3);
-        else if (lead == 1) __builtin_amdgcn_s_setprio(2);
-        else if (lead <= DPF_PRIO_FEEDBACK) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
+        prio_by_lead(c.prog, c.pslot, ++c.groups, 1, DPF_PRIO_FEEDBACK);
         return;
     }
 #endif
@@ -419,9 +433,7 @@ __global__ __launch_bounds__(kTreeBlockMax, kTreeWaves) void k_evalfull(const ui
     // kTreeBlockBig-thread workgroup per CU): with two workgroups per CU a
     // wave sees half of its SIMD's waves, and steering by them was 3% slower.
     if (UNIFORM && !NODES && D >= (int)kBigMinD && Bw == 1024u) {
-        const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);   // HW_ID: wave id [3:0], SIMD [5:4]
-        c.prog = s_prog + 16 * ((hw >> 4) & 3u);
-        c.pslot = hw & 15u;
+        c.prog = prog_slots(s_prog, c.pslot);
         c.prog[c.pslot] = 0;
     }
 #endif
@@ -918,9 +930,8 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
     fill_table(s_tab);
     __builtin_amdgcn_s_setprio(3);
 #if DPF_EVAL_FEEDBACK
-    const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);
-    uint32_t* prog = s_prog + 16 * ((hw >> 4) & 3u);
-    const uint32_t pslot = hw & 15u;
+    uint32_t pslot;
+    uint32_t* prog = prog_slots(s_prog, pslot);
     prog[pslot] = 0;
 #endif
     issue_nodes(0, 0);
@@ -932,19 +943,7 @@ __global__ __launch_bounds__(kEvalPBlock, 1) void k_eval_persist(const uint32_t*
     }
     for (uint64_t it = 0; it < iters; ++it) {
 #if DPF_EVAL_FEEDBACK
-        if ((it & 3) == 0) {
-            const uint32_t d = (uint32_t)it;
-            prog[pslot] = d;
-            const uint4* q = reinterpret_cast<const uint4*>(prog);
-            const uint4 a = q[0], b = q[1], e = q[2], f = q[3];
-            uint32_t m = min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w)));
-            m = min(m, min(min(min(e.x, e.y), min(e.z, e.w)), min(min(f.x, f.y), min(f.z, f.w))));
-            const uint32_t lead = d - __builtin_amdgcn_readfirstlane(m < d ? m : d);
-            if (lead == 0) __builtin_amdgcn_s_setprio(3);
-            else if (lead <= 4) __builtin_amdgcn_s_setprio(2);
-            else if (lead <= 4 * DPF_EVAL_FEEDBACK) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
+        if ((it & 3) == 0) prio_by_lead(prog, pslot, (uint32_t)it, 4, 4 * DPF_EVAL_FEEDBACK);   // progress: pairs walked
 #else
         if (it * 16 >= 15 * iters) __builtin_amdgcn_s_setprio(0);
         else if (it * 16 >= 14 * iters) __builtin_amdgcn_s_setprio(1);
