@@ -86,6 +86,22 @@ def test_config1_every_byte_vs_oracle(cfg1, aes, share):
     assert np.array_equal(got, want[share]), _first_diff(got, want[share])
 
 
+@pytest.mark.parametrize("nk", [2056, 4100])
+def test_big_workgroups_with_a_ragged_last_one(nk):
+    """r06: leaf launches with deep subtrees run 1024-thread workgroups whose
+    waves steer their priority by the progress of the other waves of their
+    SIMD (LDS slots, dpf_kernels.hip prio_by_lead).  At 2056 / 4100 keys the
+    grid's last workgroup is half full: its missing waves never publish
+    progress, the others must neither wait on them nor write past the batch.
+    Every byte against the oracle."""
+    logN = 20
+    al, s0, s1 = synth.key_seeds(nk, logN, first=31337)
+    ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+    got = _dev_evalfull(ka, logN)
+    want = oracle.evalfull_batch(ka, logN, nthreads=NT)
+    assert np.array_equal(got, want), _first_diff(got, want)
+
+
 def test_config1_host_buffer_api_every_byte(cfg1):
     """The drop-in host-buffer entry (dpf_evalfull_batch: staged chunks,
     kernel / D2H / host copy overlapped) at full size."""
