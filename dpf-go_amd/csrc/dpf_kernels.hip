@@ -432,7 +432,7 @@ __global__ __launch_bounds__(kTreeBlockMax, kTreeWaves) void k_evalfull(const ui
     // Only where the workgroup holds all 16 waves of its CU (one
     // kTreeBlockBig-thread workgroup per CU): with two workgroups per CU a
     // wave sees half of its SIMD's waves, and steering by them was 3% slower.
-    if (UNIFORM && !NODES && D >= (int)kBigMinD && Bw == 1024u) {
+    if (UNIFORM && !NODES && D >= (int)kFeedbackMinD && Bw == 1024u) {
         c.prog = prog_slots(s_prog, c.pslot);
         c.prog[c.pslot] = 0;
     }

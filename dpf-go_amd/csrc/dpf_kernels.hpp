@@ -28,6 +28,10 @@ constexpr int kTreeBlockMax = kTreeBlock > kTreeBlockBig ? kTreeBlock : kTreeBlo
 #define DPF_BIG_MIN_D 6
 #endif
 constexpr uint32_t kBigMinD = DPF_BIG_MIN_D;
+#ifndef DPF_FEEDBACK_MIN_D
+#define DPF_FEEDBACK_MIN_D 6
+#endif
+constexpr uint32_t kFeedbackMinD = DPF_FEEDBACK_MIN_D;   // progress feedback needs enough groups per thread
 constexpr int kTreeWaves = DPF_TREE_WAVES;
 constexpr uint32_t kMaxD = 7;  // per-thread DFS subtree depth: 128 leaves = 2 KiB of output per thread
 constexpr uint32_t kMaxFrontierHbm = 16;  // batched Eval, HBM frontier: deepest shared level
