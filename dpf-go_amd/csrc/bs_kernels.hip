@@ -25,9 +25,13 @@
 #include "aes_bytesliced.hpp"
 #include "bs_kernels.hpp"
 #include "dpf_kernels.hpp"
+#include "wave_prio.hpp"
 
 #ifndef DPF_BS_PRIO
 #define DPF_BS_PRIO 1   // issue priority by progress in k_evalfull_bs
+#endif
+#ifndef DPF_BS_FEEDBACK
+#define DPF_BS_FEEDBACK 0   // >0: 512-thread workgroups (every wave of a CU) and progress-feedback priority (A/B)
 #endif
 
 namespace dpfk {
@@ -199,7 +203,7 @@ __device__ __forceinline__ void leaf_store(uint32_t (&o)[32], uint32_t tl, const
         DST[4 * q_] = v_.x; DST[4 * q_ + 1] = v_.y; DST[4 * q_ + 2] = v_.z; DST[4 * q_ + 3] = v_.w; \
     }
 
-constexpr int kBsBlock = 256;
+constexpr int kBsBlock = DPF_BS_FEEDBACK ? 512 : 256;
 
 // Thread u: key u >> (flog - 3), frontier nodes 8*(u mod 2^(flog-3)) .. +7
 // of that key (level lvl0; 2^flog frontier nodes per key).  Output: 2^D
@@ -211,7 +215,17 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
                                                         uint32_t lvl0, uint64_t nthreads, uint8_t* __restrict__ out,
                                                         uint64_t out_stride) {
     const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+#if DPF_BS_FEEDBACK
+    __shared__ __attribute__((aligned(16))) uint32_t s_prog[64];
+    if (threadIdx.x < 64) s_prog[threadIdx.x] = 0xffffffffu;
+    __syncthreads();                               // before any wave returns or reads the slots
+    uint32_t pslot = 0;
+    uint32_t* prog = blockDim.x == 512u ? prog_slots(s_prog, pslot) : nullptr;
+#endif
     if (u >= nthreads) return;
+#if DPF_BS_FEEDBACK
+    if (prog) prog[pslot] = 0;
+#endif
     const uint32_t glog = flog - 3;
     uint64_t key = u >> glog;
     if constexpr (UNIFORM) key = __builtin_amdgcn_readfirstlane((uint32_t)key);
@@ -303,6 +317,10 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
         }
 #if DPF_BS_PRIO
         ++pairs;
+#if DPF_BS_FEEDBACK
+        if (prog) prio_by_lead(prog, pslot, pairs, 1, DPF_BS_FEEDBACK);
+        else
+#endif
         if (pairs * 8 >= 7 * kPairs) __builtin_amdgcn_s_setprio(1);
         else if (pairs * 4 >= 3 * kPairs) __builtin_amdgcn_s_setprio(2);
 #endif
@@ -319,6 +337,9 @@ __global__ __launch_bounds__(kBsBlock, 2) void k_evalfull_bs(const uint4* __rest
         }
         path |= 1u;
     }
+#if DPF_BS_FEEDBACK
+    if (prog) prog[pslot] = 0xffffffffu;   // done: no longer the slowest
+#endif
 }
 
 hipError_t launch_unpack_bs(const uint8_t* keys, uint64_t key_len, uint64_t nkeys, uint32_t stop, uint32_t* ekb,
