@@ -174,3 +174,29 @@ def test_cu_masked_streams_give_identical_results():
         torch.cuda.synchronize()
         dpf.stream_destroy(T)
         dpf.stream_destroy(F)
+
+
+def test_cu_masked_stream_big_tree_workgroups():
+    """The r06 tree geometry on a CU-limited stream: 512 keys at logN 20 on 16
+    CUs fill more than a round of 512-thread groups, so the launch takes
+    1024-thread workgroups with progress-feedback priority (several rounds
+    of them on the 16 CUs).  Every byte against the oracle."""
+    import torch
+    dev = torch.device("cuda", 0)
+    S = dpf.stream_create_cu_masked(0, 16)
+    try:
+        logN, nk = 20, 512
+        al, s0, s1 = synth.key_seeds(nk, logN, first=2626)
+        ka, _ = dpf.gen_batch_seeded(al, logN, s0, s1)
+        kl, ol = dpf.key_len(logN), dpf.evalfull_len(logN)
+        d_keys = torch.from_numpy(ka.reshape(-1)).to(dev)
+        d_work = torch.empty(dpf.workspace_size(nk, logN), dtype=torch.uint8, device=dev)
+        out = torch.full((nk * ol,), 0x5A, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        dpf.evalfull_batch_dev(d_keys, kl, nk, logN, out, d_work, stream=S)
+        S.synchronize()
+        want = oracle.evalfull_batch(ka, logN, nthreads=8)
+        assert np.array_equal(out.cpu().numpy().reshape(nk, ol), want)
+    finally:
+        torch.cuda.synchronize()
+        dpf.stream_destroy(S)
