@@ -137,8 +137,8 @@ def test_every_bound_function_is_declared_with_matching_arguments():
 
 
 def test_every_bound_function_is_exported():
-    if not os.path.exists(LIB):
-        pytest.skip("libdpf_hip.so not built (make -C dpf-go_amd)")
+    if not os.path.exists(LIB) or shutil.which("nm") is None:
+        pytest.skip("libdpf_hip.so not built (make -C dpf-go_amd) or no nm")
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
     missing = sorted({n for _, n, _, _ in go_calls()} - exported)
